@@ -1,0 +1,170 @@
+"""Generate tests/golden/ fixtures from the REFERENCE implementation (runs in the build container only).
+
+The reference tree (/root/reference, read-only) is imported here to produce input/output vectors;
+nothing from it is copied into the repo and nothing in tests/, bench.py or the engine reads it at
+run time. Re-run with:  PYTHONDONTWRITEBYTECODE=1 python scripts/make_golden.py
+
+Fixtures (all .npz, loadable with allow_pickle=False):
+  decode_tiny_{xavier,wc}.npz     FCModel._sample (src/captioning/nets.py:183-245) on tiny dims,
+                                  theta stored in full; reference seq/logprobs + top-2 margins
+  decode_full_{xavier,wc}.npz     full fc_caption dims (V=9487, E=R=128, F=2048); theta and fc are
+                                  regenerated from the stored seeds (oracle.make_theta / numpy PCG64),
+                                  plus two table-perturbed members (theta+delta, theta-delta)
+  perturb_semantics.npz           PolicyNet.evolve (src/algorithm/nets.py:83-119): new params ==
+                                  fp32(theta + delta), and worker's theta - delta (nic_nes_worker.py:151)
+  adam.npz                        Adam.update (src/algorithm/nic_nes/optimizers.py:15-22,78-83) driven
+                                  like NESMaster.run_master (nic_nes_master.py:126-133), 3 steps
+  ranks.npz                       compute_centered_ranks docstring known answer (nic_nes_master.py:187-189)
+"""
+import json
+import os
+import sys
+from collections import namedtuple
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, '/root/reference/src')
+
+from oracle import oracle as O  # noqa: E402
+
+import captioning.nets as ref_nets  # noqa: E402  (reference module)
+
+OUT = os.path.join(REPO, 'tests', 'golden')
+os.makedirs(OUT, exist_ok=True)
+torch.set_num_threads(1)          # the reference pins one thread per worker (src/main.py:8-11)
+torch.set_grad_enabled(False)
+
+Opt = namedtuple('Opt', ['vocab_size', 'input_encoding_size', 'rnn_size', 'fc_feat_size', 'vbn', 'vbn_e',
+                         'vbn_affine', 'layer_n', 'layer_n_affine', 'safe_mutations',
+                         'safe_mutation_underflow', 'safe_mutation_vector'])
+
+
+def ref_model(d):
+    opt = Opt(d.vocab_size, d.E, d.R, d.F, False, False, False, False, False, '', 0.1, '')
+    return ref_nets.FCModel(options=opt)
+
+
+def load_theta(model, theta32):
+    torch.nn.utils.vector_to_parameters(torch.from_numpy(np.ascontiguousarray(theta32)), model.parameters())
+
+
+def ref_decode(model, fc):
+    """Reference greedy decode + per-step top-2 log-prob margin (replayed with the model's own
+    modules in the same op order as FCModel._sample; the replayed tokens are asserted equal)."""
+    fct = torch.from_numpy(fc)
+    seq, slp = model._sample(fct, greedy=True)
+    B = fc.shape[0]
+    state = model.init_hidden(B)
+    margins = np.full((B, model.seq_length), np.inf, np.float32)
+    xt = model.img_embed(fct)
+    _, state = model.core(xt, state)
+    it = fct.new_zeros(B, dtype=torch.long)
+    unfinished = None
+    for t in range(1, model.seq_length + 1):
+        xt = model.embed(it)
+        out, state = model.core(xt, state)
+        lp = torch.nn.functional.log_softmax(model.logit(out), dim=1)
+        top = lp.topk(2, 1).values
+        margins[:, t - 1] = (top[:, 0] - top[:, 1]).numpy()
+        _, it = torch.max(lp, 1)
+        unfinished = (it > 0) if t == 1 else unfinished * (it > 0)
+        it = it * unfinished.type_as(it)
+        assert torch.equal(it, seq[:, t - 1]), 'replay diverged from _sample'
+        if unfinished.sum() == 0:
+            break
+    return seq.numpy().astype(np.int32), slp.numpy().astype(np.float32), margins
+
+
+def decode_fixture(name, d, theta_seed, gain, bias_std, fc_seed, B, store_theta, members=()):
+    model = ref_model(d)
+    theta = O.make_theta(d, theta_seed, gain, bias_std)
+    fc = np.random.Generator(np.random.PCG64(fc_seed)).standard_normal((B, d.F)).astype(np.float32)
+    load_theta(model, theta)
+    seq, slp, mar = ref_decode(model, fc)
+    out = dict(dims=np.array([d.vocab_size, d.E, d.R, d.F, d.T], np.int64),
+               theta_seed=np.int64(theta_seed), gain=np.float64(gain), bias_std=np.float64(bias_std),
+               fc_seed=np.int64(fc_seed), B=np.int64(B), seq=seq, logprobs=slp, margins=mar)
+    if store_theta:
+        out['theta'] = theta
+        out['fc'] = fc
+    # table-perturbed members (theta +- fp32(sigma z)), the engine's noise contract
+    if members:
+        T, tseed, nseed, it, sigma = 1 << 23, 123, 7, 3, 0.01
+        table = O.noise_table(T, tseed)
+        out.update(noise_len=np.int64(T), table_seed=np.int64(tseed), noise_seed=np.int64(nseed),
+                   iteration=np.int64(it), sigma=np.float64(sigma), members=np.array(members, np.int64))
+        pseq, pmar = [], []
+        for mbr in members:
+            idx = O.noise_index(nseed, it, mbr, T, d.D)
+            for sign in (+1, -1):
+                load_theta(model, O.perturb(theta, table, idx, sigma, sign))
+                s, _, m = ref_decode(model, fc)
+                pseq.append(s)
+                pmar.append(m)
+        out['member_seq'] = np.stack(pseq)       # [members*2, B, T] order (m0+, m0-, m1+, ...)
+        out['member_margins'] = np.stack(pmar)
+    np.savez_compressed(os.path.join(OUT, name + '.npz'), **out)
+    print(name, 'seq[0]', seq[0], 'min margin', float(mar.min()))
+
+
+def perturb_fixture():
+    d = O.Dims(vocab_size=63, E=32, R=32, F=64)
+    model = ref_model(d)
+    theta = O.make_theta(d, 5)
+    load_theta(model, theta)
+    torch.manual_seed(11)
+    delta = model.evolve(0.01)                                     # reference PolicyNet.evolve
+    plus = torch.nn.utils.parameters_to_vector(model.parameters()).numpy().copy()
+    minus = (torch.from_numpy(theta) - torch.from_numpy(delta)).numpy()   # nic_nes_worker.py:151
+    np.savez_compressed(os.path.join(OUT, 'perturb_semantics.npz'), theta=theta, delta=delta, plus=plus,
+                        minus=minus)
+    print('perturb: plus==theta+delta', bool(np.array_equal(plus, theta + delta)))
+
+
+def adam_fixture():
+    np.float = float        # numpy>=1.24 removed the alias optimizers.py:75-76 uses
+    from algorithm.nic_nes.optimizers import Adam   # reference module
+    rng = np.random.Generator(np.random.PCG64(99))
+    D = 1000
+    theta32 = rng.standard_normal(D).astype(np.float32)
+    grads = rng.standard_normal((3, D)).astype(np.float32) * np.float32(0.05)
+    l2coeff, stepsize = 1e-3, 1e-2
+    opt = Adam(theta32.copy(), stepsize)
+    theta = theta32.copy()
+    thetas, ratios, ms, vs = [], [], [], []
+    for k in range(3):
+        reg = l2coeff * theta                    # nic_nes_master.py:311 restated (fp32 first step)
+        ratio, theta = opt.update(-grads[k] + reg)
+        thetas.append(np.asarray(theta, np.float64))
+        ratios.append(ratio)
+        ms.append(opt.m.copy())
+        vs.append(opt.v.copy())
+    np.savez_compressed(os.path.join(OUT, 'adam.npz'), theta0=theta32, grads=grads, l2coeff=np.float64(l2coeff),
+                        stepsize=np.float64(stepsize), thetas=np.stack(thetas), ratios=np.array(ratios),
+                        ms=np.stack(ms), vs=np.stack(vs))
+    print('adam ok, ratio', ratios)
+
+
+def ranks_fixture():
+    # docstring known answer, /root/reference/src/algorithm/nic_nes/nic_nes_master.py:187-189
+    x = np.array([[101, 200], [2, 100]], np.float64)
+    y = np.array([[0.16666667, 0.5], [-0.5, -0.16666667]])
+    np.savez_compressed(os.path.join(OUT, 'ranks.npz'), x=x, y=y)
+
+
+if __name__ == '__main__':
+    tiny = O.Dims(vocab_size=63, E=32, R=32, F=64)
+    full = O.Dims()
+    decode_fixture('decode_tiny_xavier', tiny, 1, 1.0, 0.0, 1234, 8, True)
+    decode_fixture('decode_tiny_wc', tiny, 2, 4.0, 0.1, 1234, 8, True)
+    decode_fixture('decode_full_xavier', full, 0, 1.0, 0.0, 1234, 16, False, members=(0, 1))
+    decode_fixture('decode_full_wc', full, 0, 4.0, 0.1, 1234, 16, False, members=(0, 1))
+    perturb_fixture()
+    adam_fixture()
+    ranks_fixture()
+    with open(os.path.join(OUT, 'MANIFEST.json'), 'w') as f:
+        json.dump({'generator': 'scripts/make_golden.py', 'reference': 'rubencart/NES-img-captioning @ /root/reference',
+                   'torch': torch.__version__, 'numpy': np.__version__, 'threads': 1}, f, indent=1)
