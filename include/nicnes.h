@@ -1,0 +1,118 @@
+/*
+ * nicnes.h -- C ABI of the MI355X NIC-NES population-evaluation engine (libnicnes.so).
+ *
+ * Plain C: status codes, raw pointers and sizes, no torch types. All array arguments are
+ * DEVICE pointers on the handle's GPU unless the name ends in _host. `stream` is a
+ * hipStream_t (NULL = the default stream); every call only enqueues work on it, except the
+ * functions documented as synchronising. A handle is not thread-safe: one owner thread per
+ * handle, one handle per GPU. Buffers passed to nicnes_set_* are borrowed (the caller keeps
+ * them alive and unchanged until the handle is destroyed or the buffer is replaced); output
+ * buffers are written by the enqueued work.
+ *
+ * Each entry point names the reference interface (rubencart/NES-img-captioning, file:line) it
+ * replaces. Integration stubs for the reference side: INTEGRATION.md.
+ */
+#ifndef NICNES_H
+#define NICNES_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NICNES_OK 0
+#define NICNES_ERR_INVALID 1       /* bad argument / wrong state */
+#define NICNES_ERR_UNSUPPORTED 2   /* experiment option the engine does not implement */
+#define NICNES_ERR_HIP 3           /* HIP runtime error (message in nicnes_last_error) */
+#define NICNES_ERR_NOMEM 4
+
+typedef struct nicnes_handle nicnes_handle;
+
+/* Filled from the experiment JSON (src/algorithm/policies.py:31-41 ModelOptions,
+ * src/captioning/experiment.py:27-30 vocab injection, src/algorithm/tools/utils.py:14-20 Config). */
+typedef struct nicnes_config {
+    int32_t vocab_size;           /* V; logits are V + 1 wide (src/captioning/nets.py:151-152) */
+    int32_t input_encoding_size;  /* E (must be 128) */
+    int32_t rnn_size;             /* R (must be 128) */
+    int32_t fc_feat_size;         /* F (multiple of 128) */
+    int32_t seq_length;           /* 16 (src/captioning/nets.py:147) */
+    int32_t max_batch;            /* max unique images per batch (config.batch_size) */
+    int32_t max_refs;             /* max reference captions per batch */
+    int32_t max_members;          /* max population members per nicnes_evaluate call */
+    uint64_t noise_len;           /* entries of the shared Gaussian table */
+    uint64_t noise_seed;          /* seed of the member -> table-offset rule */
+} nicnes_config;
+
+/* flat parameter count D for a config (src/algorithm/nets.py:146-148 count_parameters) */
+int64_t nicnes_param_count(const nicnes_config* cfg);
+/* offsets of the 9 tensors in the flat theta (registration order) + D at [9] */
+int nicnes_param_offsets(const nicnes_config* cfg, int64_t* out10_host);
+
+int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out);
+int nicnes_destroy(nicnes_handle* h);
+const char* nicnes_last_error(const nicnes_handle* h);
+
+/* Shared noise table (borrowed), replaces the per-worker torch.normal_ draw of
+ * PolicyNet.evolve, src/algorithm/nets.py:101-102. */
+int nicnes_set_noise_table(nicnes_handle* h, const float* table, uint64_t len);
+
+/* Current parameters (copied into the engine's fp64 master + fp32 evaluation copy), replaces
+ * Policy.set_model / set_from_parameter_vector, src/algorithm/policies.py:106-147.
+ * is_fp32_origin = 1 keeps the reference's fp32-theta semantics for the first Adam step. */
+int nicnes_set_theta(nicnes_handle* h, const double* theta64, int is_fp32_origin, void* stream);
+int nicnes_get_theta(nicnes_handle* h, double* theta64_out, float* theta32_out, void* stream);
+/* Adam state in the reference layout (src/algorithm/nic_nes/optimizers.py:85-107): m, v, t */
+int nicnes_set_adam_state(nicnes_handle* h, const double* m, const double* v, int64_t t, void* stream);
+int nicnes_get_adam_state(nicnes_handle* h, double* m_out, double* v_out, int64_t* t_out_host, void* stream);
+
+/* One batch (src/captioning/dataloader.py:135-203 get_batch, deduplicated to unique images):
+ * fc [B, F] fp32; ref_tokens [n_refs, seq_length] int32 zero-padded label rows;
+ * img_ref_start [B + 1] (refs of image b are [img_ref_start[b], img_ref_start[b+1])).
+ * Builds the reference-side CIDEr-D vectors on `stream`. */
+int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t* ref_tokens, int32_t n_refs,
+                     const int32_t* img_ref_start, void* stream);
+
+/* Fixed document-frequency table (CiderD(df='coco-train-idxs'), src/captioning/policies.py:72):
+ * sorted packed n-gram keys (n<<56 | t0<<42 | t1<<28 | t2<<14 | t3), df counts, and
+ * ref_len = log(raw ref_len) as the scorer uses it. */
+int nicnes_set_df_table(nicnes_handle* h, const uint64_t* keys, const double* df, int64_t n, double ref_len_log);
+
+/* Noise-table offsets of members [member_begin, member_begin + count) at `iteration`. */
+int nicnes_noise_indices(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, uint64_t* out,
+                         void* stream);
+
+/* Evaluate `count` members (each an antithetic pair theta +- sigma z): greedy decode of the
+ * batch + CIDEr-D fitness. Replaces NESWorker.fitness (src/algorithm/nic_nes/nic_nes_worker.py:115-161)
+ * for a whole population slice. fitness_out [count, 2] fp64 = (f+, f-) per member;
+ * seq_out [count, 2, B, seq_length] int32 or NULL. */
+int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
+                    double* fitness_out, int32_t* seq_out, void* stream);
+
+/* Centred ranks + antithetic weights over the WHOLE population, replaces
+ * NESMaster.compute_centered_ranks and the weights line of gradient_estimate
+ * (src/algorithm/nic_nes/nic_nes_master.py:170-205). fitness [P, 2] fp64 -> cr [P, 2] (or NULL),
+ * w [P] fp32. */
+int nicnes_rank_weights(nicnes_handle* h, const double* fitness, int32_t P, double* cr_out, float* w_out, void* stream);
+
+/* gsum = sum over members [member_begin, +count) of w[i] * delta_i (fp32 result of an fp64 sum);
+ * replaces batched_weighted_sum (nic_nes_master.py:207-221) without materialising delta.
+ * `w` points at the weights of member_begin. Multi-GPU: all-reduce gsum between the call
+ * and nicnes_adam_step. */
+int nicnes_grad_partial(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, const float* w,
+                        float sigma, float* gsum_out, void* stream);
+
+/* g = gsum / (2P); globalg = -g + l2coeff * theta; Adam step on the engine's theta
+ * (nic_nes_master.py:126-137, optimizers.py:15-22,78-83). Synchronising: returns the
+ * update ratio |step| / |theta_old| in *ratio_out_host. */
+int nicnes_adam_step(nicnes_handle* h, const float* gsum, int32_t P, double l2coeff, double stepsize, double beta1,
+                     double beta2, double epsilon, double* ratio_out_host, void* stream);
+
+/* diagnostics: [0] = exact-pass fallbacks of the greedy tie rule since creation (synchronising) */
+int nicnes_stats(nicnes_handle* h, int64_t* out4_host);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NICNES_H */

@@ -1,0 +1,22 @@
+// Internal (non-ABI) interface of the CIDEr-D kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct CiderTables {
+    const uint64_t* df_keys;   // sorted packed n-gram keys of the document-frequency table
+    const double* df_vals;     // document frequency per key
+    int64_t df_n;
+    double ref_len;            // log(ref_len_raw)  (CiderScorer fixed-df mode)
+    // per-reference vectors (written by nicnes_cook_refs_kernel)
+    uint64_t* ref_keys;        // [n_refs, 64] distinct n-grams
+    double* ref_vec;           // [n_refs, 64] tf * idf
+    int32_t* ref_count;        // [n_refs]
+    int32_t* ref_len2;         // [n_refs] bigram count
+    double* ref_norm;          // [n_refs, 4]
+};
+
+extern "C" hipError_t nicnes_launch_cook_refs(const int32_t* ref_tokens, int n_refs, int T, const CiderTables* tb,
+                                              hipStream_t stream);
+extern "C" hipError_t nicnes_launch_cider(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
+                                          const int32_t* img_ref_start, double* fitness_out, hipStream_t stream);

@@ -1,0 +1,22 @@
+// Internal (non-ABI) launch interfaces of the engine's kernels.
+#pragma once
+#define SCR_SLOTS (64 + 64 + 320)   // per lane: c | h' | 20 partial gate tiles
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct DecodeParams {
+    const float* theta;          // base theta, fp32 [D] (flat order: SURVEY.md Appendix A.1)
+    const float* noise;          // shared Gaussian table, fp32 [noise_len]
+    const uint64_t* noise_idx;   // per member slice start (multiple of 64)
+    const float* fc;             // unique-image fc features [B, F]
+    int32_t* seq;                // out: [members, 2, B, T] greedy tokens (masked after the first 0)
+    float* scratch;              // nicnes_decode_scratch_floats(): lane-private c | h' | gate partials
+    int32_t* stats;              // [0] = exact-pass fallbacks (atomic)
+    float sigma;
+    int32_t B, F, V1, T;
+    int64_t D;
+    int64_t off_img_w, off_img_b, off_emb_w, off_log_w, off_log_b, off_i2h_w, off_i2h_b, off_h2h_w, off_h2h_b;
+};
+
+extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream);
+extern "C" size_t nicnes_decode_scratch_floats(int member_count, int nslabs);

@@ -1,0 +1,415 @@
+// engine.cpp -- the C ABI of libnicnes (include/nicnes.h): handle state, validation, launches.
+//
+// Host-side orchestration only; the arithmetic lives in decode_kernel.hip, cider_kernel.hip and
+// update_kernels.hip. Nothing here allocates or synchronises inside nicnes_evaluate /
+// nicnes_grad_partial / nicnes_rank_weights, so a caller may capture them in a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/nicnes.h"
+#include "cider_kernel.h"
+#include "decode_kernel.h"
+#include "update_kernels.h"
+
+struct nicnes_handle {
+    nicnes_config cfg;
+    int device = 0;
+    std::string err;
+    int64_t off[10];
+    int64_t D = 0;
+    int32_t V1 = 0;
+
+    const float* noise = nullptr;
+    uint64_t noise_len = 0;
+
+    double* theta64 = nullptr;
+    float* theta32 = nullptr;
+    double* m = nullptr;
+    double* v = nullptr;
+    int64_t t = 0;
+    int theta_is_fp32 = 0;
+    bool theta_set = false;
+
+    const float* fc = nullptr;
+    int32_t B = 0;
+    int32_t n_refs = 0;
+    const int32_t* img_ref_start = nullptr;
+    bool batch_set = false;
+
+    const uint64_t* df_keys = nullptr;
+    const double* df_vals = nullptr;
+    int64_t df_n = 0;
+    double ref_len = 0.0;
+    bool df_set = false;
+
+    uint64_t* ref_keys = nullptr;
+    double* ref_vec = nullptr;
+    int32_t* ref_count = nullptr;
+    int32_t* ref_len2 = nullptr;
+    double* ref_norm = nullptr;
+
+    uint64_t* nidx = nullptr;
+    int32_t* seq = nullptr;
+    float* dscratch = nullptr;
+    int32_t* stats = nullptr;
+    double* partials = nullptr;
+    double* norms = nullptr;
+};
+
+namespace {
+
+int fail(nicnes_handle* h, int code, const std::string& msg) {
+    if (h) h->err = msg;
+    return code;
+}
+
+#define HIPC(h, expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail((h), NICNES_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+void layout(const nicnes_config* c, int64_t* off) {
+    const int64_t V1 = (int64_t)c->vocab_size + 1, E = c->input_encoding_size, R = c->rnn_size,
+                  F = c->fc_feat_size;
+    int64_t o = 0;
+    off[0] = o; o += E * F;        // img_embed.weight
+    off[1] = o; o += E;            // img_embed.bias
+    off[2] = o; o += V1 * E;       // embed.weight
+    off[3] = o; o += V1 * R;       // logit.weight
+    off[4] = o; o += V1;           // logit.bias
+    off[5] = o; o += 5 * R * E;    // core.i2h.weight
+    off[6] = o; o += 5 * R;        // core.i2h.bias
+    off[7] = o; o += 5 * R * R;    // core.h2h.weight
+    off[8] = o; o += 5 * R;        // core.h2h.bias
+    off[9] = o;
+}
+
+__global__ void f64_to_f32_kernel(const double* in, float* out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (float)in[i];
+}
+
+int nslabs_of(int B) { return (B + 127) / 128; }
+
+template <class T>
+int dalloc(nicnes_handle* h, T** p, size_t n) {
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+    if (e != hipSuccess) return fail(h, NICNES_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return NICNES_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t nicnes_param_count(const nicnes_config* cfg) {
+    if (!cfg) return -1;
+    int64_t off[10];
+    layout(cfg, off);
+    return off[9];
+}
+
+int nicnes_param_offsets(const nicnes_config* cfg, int64_t* out10_host) {
+    if (!cfg || !out10_host) return NICNES_ERR_INVALID;
+    layout(cfg, out10_host);
+    return NICNES_OK;
+}
+
+int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
+    if (!cfg || !out) return NICNES_ERR_INVALID;
+    *out = nullptr;
+    const int V1 = cfg->vocab_size + 1;
+    if (cfg->input_encoding_size != 128 || cfg->rnn_size != 128) return NICNES_ERR_UNSUPPORTED;
+    if (cfg->fc_feat_size <= 0 || cfg->fc_feat_size % 128 != 0) return NICNES_ERR_UNSUPPORTED;
+    if (V1 % 4 != 0 || V1 < 8 || V1 > 16384) return NICNES_ERR_UNSUPPORTED;
+    if (cfg->seq_length < 1 || cfg->seq_length > 16) return NICNES_ERR_UNSUPPORTED;
+    if (cfg->max_batch < 1 || cfg->max_batch > 1024 || cfg->max_members < 1 || cfg->max_refs < 1)
+        return NICNES_ERR_INVALID;
+    nicnes_handle* h = new nicnes_handle();
+    h->cfg = *cfg;
+    h->device = device;
+    h->V1 = V1;
+    layout(cfg, h->off);
+    h->D = h->off[9];
+    if (h->D * 4 >= (int64_t)1 << 32) {
+        delete h;
+        return NICNES_ERR_UNSUPPORTED;
+    }
+    if (cfg->noise_len < (uint64_t)h->D) {
+        delete h;
+        return NICNES_ERR_INVALID;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        delete h;
+        return NICNES_ERR_HIP;
+    }
+    const size_t D = (size_t)h->D, MR = (size_t)cfg->max_refs, MM = (size_t)cfg->max_members,
+                 MB = (size_t)cfg->max_batch, T = (size_t)cfg->seq_length;
+    int rc = NICNES_OK;
+    if (!rc) rc = dalloc(h, &h->theta64, D);
+    if (!rc) rc = dalloc(h, &h->theta32, D);
+    if (!rc) rc = dalloc(h, &h->m, D);
+    if (!rc) rc = dalloc(h, &h->v, D);
+    if (!rc) rc = dalloc(h, &h->ref_keys, MR * 64);
+    if (!rc) rc = dalloc(h, &h->ref_vec, MR * 64);
+    if (!rc) rc = dalloc(h, &h->ref_count, MR);
+    if (!rc) rc = dalloc(h, &h->ref_len2, MR);
+    if (!rc) rc = dalloc(h, &h->ref_norm, MR * 4);
+    if (!rc) rc = dalloc(h, &h->nidx, MM);
+    if (!rc) rc = dalloc(h, &h->seq, MM * 2 * MB * T);
+    if (!rc) rc = dalloc(h, &h->dscratch, nicnes_decode_scratch_floats((int)MM, nslabs_of((int)MB)));
+    if (!rc) rc = dalloc(h, &h->stats, 4);
+    if (!rc) rc = dalloc(h, &h->partials, 2 * (size_t)nicnes_adam_blocks(h->D));
+    if (!rc) rc = dalloc(h, &h->norms, 2);
+    if (rc) {
+        nicnes_destroy(h);
+        return rc;
+    }
+    (void)hipMemset(h->m, 0, D * sizeof(double));
+    (void)hipMemset(h->v, 0, D * sizeof(double));
+    (void)hipMemset(h->stats, 0, 4 * sizeof(int32_t));
+    if (hipDeviceSynchronize() != hipSuccess) {
+        nicnes_destroy(h);
+        return NICNES_ERR_HIP;
+    }
+    *out = h;
+    return NICNES_OK;
+}
+
+int nicnes_destroy(nicnes_handle* h) {
+    if (!h) return NICNES_OK;
+    (void)hipSetDevice(h->device);
+    void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
+                    h->ref_norm, h->nidx, h->seq, h->dscratch, h->stats, h->partials, h->norms};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    delete h;
+    return NICNES_OK;
+}
+
+const char* nicnes_last_error(const nicnes_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int nicnes_set_noise_table(nicnes_handle* h, const float* table, uint64_t len) {
+    if (!h || !table) return NICNES_ERR_INVALID;
+    if (len != h->cfg.noise_len) return fail(h, NICNES_ERR_INVALID, "noise table length != config.noise_len");
+    if (((uintptr_t)table & 15u) != 0) return fail(h, NICNES_ERR_INVALID, "noise table must be 16-byte aligned");
+    h->noise = table;
+    h->noise_len = len;
+    return NICNES_OK;
+}
+
+int nicnes_set_theta(nicnes_handle* h, const double* theta64, int is_fp32_origin, void* stream) {
+    if (!h || !theta64) return NICNES_ERR_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, hipMemcpyAsync(h->theta64, theta64, (size_t)h->D * sizeof(double), hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(f64_to_f32_kernel, dim3((unsigned)((h->D + 255) / 256)), dim3(256), 0, s, h->theta64,
+                       h->theta32, h->D);
+    HIPC(h, hipGetLastError());
+    h->theta_is_fp32 = is_fp32_origin ? 1 : 0;
+    h->theta_set = true;
+    return NICNES_OK;
+}
+
+int nicnes_get_theta(nicnes_handle* h, double* theta64_out, float* theta32_out, void* stream) {
+    if (!h || !h->theta_set) return NICNES_ERR_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    if (theta64_out)
+        HIPC(h, hipMemcpyAsync(theta64_out, h->theta64, (size_t)h->D * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (theta32_out)
+        HIPC(h, hipMemcpyAsync(theta32_out, h->theta32, (size_t)h->D * sizeof(float), hipMemcpyDeviceToDevice, s));
+    return NICNES_OK;
+}
+
+int nicnes_set_adam_state(nicnes_handle* h, const double* m, const double* v, int64_t t, void* stream) {
+    if (!h || !m || !v || t < 0) return NICNES_ERR_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, hipMemcpyAsync(h->m, m, (size_t)h->D * sizeof(double), hipMemcpyDeviceToDevice, s));
+    HIPC(h, hipMemcpyAsync(h->v, v, (size_t)h->D * sizeof(double), hipMemcpyDeviceToDevice, s));
+    h->t = t;
+    return NICNES_OK;
+}
+
+int nicnes_get_adam_state(nicnes_handle* h, double* m_out, double* v_out, int64_t* t_out_host, void* stream) {
+    if (!h) return NICNES_ERR_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    if (m_out) HIPC(h, hipMemcpyAsync(m_out, h->m, (size_t)h->D * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (v_out) HIPC(h, hipMemcpyAsync(v_out, h->v, (size_t)h->D * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (t_out_host) *t_out_host = h->t;
+    return NICNES_OK;
+}
+
+static CiderTables tables_of(nicnes_handle* h) {
+    CiderTables tb;
+    tb.df_keys = h->df_keys;
+    tb.df_vals = h->df_vals;
+    tb.df_n = h->df_n;
+    tb.ref_len = h->ref_len;
+    tb.ref_keys = h->ref_keys;
+    tb.ref_vec = h->ref_vec;
+    tb.ref_count = h->ref_count;
+    tb.ref_len2 = h->ref_len2;
+    tb.ref_norm = h->ref_norm;
+    return tb;
+}
+
+int nicnes_set_df_table(nicnes_handle* h, const uint64_t* keys, const double* df, int64_t n, double ref_len_log) {
+    if (!h || n < 0 || (n > 0 && (!keys || !df))) return NICNES_ERR_INVALID;
+    h->df_keys = keys;
+    h->df_vals = df;
+    h->df_n = n;
+    h->ref_len = ref_len_log;
+    h->df_set = true;
+    h->batch_set = false;   // reference vectors depend on the df table: set the batch again
+    return NICNES_OK;
+}
+
+int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t* ref_tokens, int32_t n_refs,
+                     const int32_t* img_ref_start, void* stream) {
+    if (!h || !fc || !ref_tokens || !img_ref_start) return NICNES_ERR_INVALID;
+    if (B < 1 || B > h->cfg.max_batch) return fail(h, NICNES_ERR_INVALID, "B out of [1, max_batch]");
+    if (n_refs < B || n_refs > h->cfg.max_refs) return fail(h, NICNES_ERR_INVALID, "n_refs out of [B, max_refs]");
+    if (!h->df_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_df_table first");
+    if (((uintptr_t)fc & 15u) != 0) return fail(h, NICNES_ERR_INVALID, "fc must be 16-byte aligned");
+    HIPC(h, hipSetDevice(h->device));
+    h->fc = fc;
+    h->B = B;
+    h->n_refs = n_refs;
+    h->img_ref_start = img_ref_start;
+    CiderTables tb = tables_of(h);
+    HIPC(h, nicnes_launch_cook_refs(ref_tokens, n_refs, h->cfg.seq_length, &tb, (hipStream_t)stream));
+    h->batch_set = true;
+    return NICNES_OK;
+}
+
+int nicnes_noise_indices(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, uint64_t* out,
+                         void* stream) {
+    if (!h || !out || member_begin < 0 || count < 0) return NICNES_ERR_INVALID;
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, nicnes_launch_noise_index(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, h->cfg.noise_len,
+                                      (uint64_t)h->D, out, (hipStream_t)stream));
+    return NICNES_OK;
+}
+
+int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
+                    double* fitness_out, int32_t* seq_out, void* stream) {
+    if (!h || !fitness_out || member_begin < 0) return NICNES_ERR_INVALID;
+    if (count < 1 || count > h->cfg.max_members) return fail(h, NICNES_ERR_INVALID, "count out of [1, max_members]");
+    if (!h->noise) return fail(h, NICNES_ERR_INVALID, "nicnes_set_noise_table first");
+    if (!h->theta_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_theta first");
+    if (!h->batch_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_batch first");
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, nicnes_launch_noise_index(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, h->cfg.noise_len,
+                                      (uint64_t)h->D, h->nidx, s));
+    DecodeParams p;
+    p.theta = h->theta32;
+    p.noise = h->noise;
+    p.noise_idx = h->nidx;
+    p.fc = h->fc;
+    p.seq = seq_out ? seq_out : h->seq;
+    p.scratch = h->dscratch;
+    p.stats = h->stats;
+    p.sigma = sigma;
+    p.B = h->B;
+    p.F = h->cfg.fc_feat_size;
+    p.V1 = h->V1;
+    p.T = h->cfg.seq_length;
+    p.D = h->D;
+    p.off_img_w = h->off[0];
+    p.off_img_b = h->off[1];
+    p.off_emb_w = h->off[2];
+    p.off_log_w = h->off[3];
+    p.off_log_b = h->off[4];
+    p.off_i2h_w = h->off[5];
+    p.off_i2h_b = h->off[6];
+    p.off_h2h_w = h->off[7];
+    p.off_h2h_b = h->off[8];
+    // rows a member never writes (all finished early) must read as 0 (nets.py:188 zeros)
+    HIPC(h, hipMemsetAsync(p.seq, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(int32_t), s));
+    HIPC(h, nicnes_launch_decode(&p, count, nslabs_of(h->B), s));
+    CiderTables tb = tables_of(h);
+    HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, fitness_out, s));
+    return NICNES_OK;
+}
+
+int nicnes_rank_weights(nicnes_handle* h, const double* fitness, int32_t P, double* cr_out, float* w_out, void* stream) {
+    if (!h || !fitness || !w_out || P < 1) return NICNES_ERR_INVALID;
+    if (P > 5120) return fail(h, NICNES_ERR_UNSUPPORTED, "P > 5120");
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, nicnes_launch_rank(fitness, 2 * P, cr_out, w_out, (hipStream_t)stream));
+    return NICNES_OK;
+}
+
+int nicnes_grad_partial(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, const float* w,
+                        float sigma, float* gsum_out, void* stream) {
+    if (!h || !w || !gsum_out || member_begin < 0 || count < 0) return NICNES_ERR_INVALID;
+    if (count > h->cfg.max_members) return fail(h, NICNES_ERR_INVALID, "count > max_members");
+    if (!h->noise) return fail(h, NICNES_ERR_INVALID, "nicnes_set_noise_table first");
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, nicnes_launch_noise_index(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, h->cfg.noise_len,
+                                      (uint64_t)h->D, h->nidx, s));
+    HIPC(h, nicnes_launch_grad(h->noise, h->nidx, w, count, sigma, h->D, gsum_out, s));
+    return NICNES_OK;
+}
+
+int nicnes_adam_step(nicnes_handle* h, const float* gsum, int32_t P, double l2coeff, double stepsize, double beta1,
+                     double beta2, double epsilon, double* ratio_out_host, void* stream) {
+    if (!h || !gsum || P < 1) return NICNES_ERR_INVALID;
+    if (!h->theta_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_theta first");
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    h->t += 1;
+    AdamParams p;
+    p.theta64 = h->theta64;
+    p.theta32 = h->theta32;
+    p.m = h->m;
+    p.v = h->v;
+    p.gsum = gsum;
+    p.partials = h->partials;
+    p.dim = h->D;
+    p.two_f = (float)(2 * P);
+    p.theta_is_fp32 = h->theta_is_fp32;
+    p.l2coeff = l2coeff;
+    p.l2coeff32 = (float)l2coeff;
+    // a = stepsize * sqrt(1 - b2^t) / (1 - b1^t)   (optimizers.py:79, Python float arithmetic)
+    p.a = stepsize * std::sqrt(1.0 - std::pow(beta2, (double)h->t)) / (1.0 - std::pow(beta1, (double)h->t));
+    p.beta1 = beta1;
+    p.beta2 = beta2;
+    p.one_minus_beta1 = 1.0 - beta1;
+    p.one_minus_beta2 = 1.0 - beta2;
+    p.one_minus_beta1_32 = (float)(1.0 - beta1);
+    p.one_minus_beta2_32 = (float)(1.0 - beta2);
+    p.epsilon = epsilon;
+    HIPC(h, nicnes_launch_adam(&p, h->norms, s));
+    h->theta_is_fp32 = 0;
+    if (ratio_out_host) {
+        double n2[2];
+        HIPC(h, hipMemcpyAsync(n2, h->norms, sizeof n2, hipMemcpyDeviceToHost, s));
+        HIPC(h, hipStreamSynchronize(s));
+        *ratio_out_host = std::sqrt(n2[0]) / std::sqrt(n2[1]);
+    }
+    return NICNES_OK;
+}
+
+int nicnes_stats(nicnes_handle* h, int64_t* out4_host) {
+    if (!h || !out4_host) return NICNES_ERR_INVALID;
+    int32_t st[4];
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, hipMemcpy(st, h->stats, sizeof st, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 4; ++i) out4_host[i] = st[i];
+    return NICNES_OK;
+}
+
+}  // extern "C"

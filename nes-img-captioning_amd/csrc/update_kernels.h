@@ -1,0 +1,29 @@
+// Internal (non-ABI) interface of the master-side kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct AdamParams {
+    double* theta64;        // fp64 master theta (updated in place)
+    float* theta32;         // fp32 evaluation copy (written)
+    double* m;
+    double* v;
+    const float* gsum;      // sum over members of w_i * delta_i (all ranks), fp32
+    double* partials;       // [2 * nicnes_adam_blocks(dim)]
+    int64_t dim;
+    float two_f;            // 2F: ranked_fitnesses.size
+    int32_t theta_is_fp32;  // 1 before the first update (reference theta is still fp32)
+    double l2coeff;
+    float l2coeff32;
+    double a;               // stepsize * sqrt(1 - b2^t) / (1 - b1^t), computed on the host
+    double beta1, beta2, one_minus_beta1, one_minus_beta2, epsilon;
+    float one_minus_beta1_32, one_minus_beta2_32;
+};
+
+extern "C" hipError_t nicnes_launch_noise_index(uint64_t seed, uint64_t iteration, uint64_t member0, int count,
+                                                uint64_t table_len, uint64_t dim, uint64_t* out, hipStream_t s);
+extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, double* cr_out, float* w_out, hipStream_t s);
+extern "C" hipError_t nicnes_launch_grad(const float* noise, const uint64_t* idx, const float* w, int count, float sigma,
+                                         int64_t dim, float* gsum, hipStream_t s);
+extern "C" int nicnes_adam_blocks(int64_t dim);
+extern "C" hipError_t nicnes_launch_adam(const AdamParams* p, double* norms_out, hipStream_t s);

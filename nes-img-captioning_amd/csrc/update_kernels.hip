@@ -1,0 +1,189 @@
+// update_kernels.hip -- master side of one NIC-NES iteration on gfx950.
+//
+//   noise indices          new contract replacing the shipped noise vectors
+//                          (nic_nes_worker.py:142,156-161; include/nicnes_math.h nn_noise_index)
+//   centred ranks          NESMaster.compute_ranks / compute_centered_ranks (nic_nes_master.py:184-205),
+//                          stable (value, index) order
+//   weighted noise sum     NESMaster.gradient_estimate + batched_weighted_sum (nic_nes_master.py:170-221),
+//                          delta_i re-read from the table, fp64 accumulation in member order
+//   Adam                   Optimizer.update + Adam._compute_step (optimizers.py:15-22,78-83) with the
+//                          master's g' = -g + l2coeff*theta (nic_nes_master.py:126,133), fp64 state,
+//                          evaluated with the same IEEE op sequence numpy uses (no fma contraction)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nicnes_math.h"
+#include "update_kernels.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ void nicnes_noise_index_kernel(uint64_t seed, uint64_t iteration, uint64_t member0, int count,
+                                          uint64_t table_len, uint64_t dim, uint64_t* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) out[i] = nn_noise_index(seed, iteration, member0 + (uint64_t)i, table_len, dim);
+}
+
+// rank_i = #{j : x_j < x_i} + #{j < i : x_j == x_i}  over the ravelled (P, 2) fitness
+__global__ __launch_bounds__(1024) void nicnes_rank_kernel(const double* fit, int n, double* cr_out, float* w_out) {
+    extern __shared__ double xs[];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) xs[i] = fit[i];
+    __syncthreads();
+    double* crs = xs + n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const double xi = xs[i];
+        int rank = 0;
+        for (int j = 0; j < n; ++j) {
+            const double xj = xs[j];
+            rank += (xj < xi) || (xj == xi && j < i);
+        }
+        double y = (double)rank;
+        y /= (double)(n - 1);                  // y /= (x.size - 1)
+        y -= 0.5;                              // y -= .5
+        crs[i] = y;
+        if (cr_out) cr_out[i] = y;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < n / 2; p += blockDim.x)
+        w_out[p] = (float)(crs[2 * p] - crs[2 * p + 1]);     // cr[:, 0] - cr[:, 1], then fp32 dot
+}
+
+// gsum[j] = fp32( sum_i w_i * fp32(sigma * z[idx_i + j]) ), fp64 accumulation in member order
+__global__ __launch_bounds__(256) void nicnes_grad_kernel(const float* noise, const uint64_t* idx, const float* w,
+                                                          int count, float sigma, int64_t dim, float* gsum) {
+    const int64_t j4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (j4 >= dim) return;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const bool full = j4 + 4 <= dim;
+    for (int i = 0; i < count; ++i) {
+        const float* z = noise + idx[i] + j4;
+        const double wi = (double)w[i];
+        if (full) {
+            const f32x4 zz = *reinterpret_cast<const f32x4*>(z);
+            a0 += wi * (double)(sigma * zz[0]);
+            a1 += wi * (double)(sigma * zz[1]);
+            a2 += wi * (double)(sigma * zz[2]);
+            a3 += wi * (double)(sigma * zz[3]);
+        } else {
+            a0 += wi * (double)(sigma * z[0]);
+            if (j4 + 1 < dim) a1 += wi * (double)(sigma * z[1]);
+            if (j4 + 2 < dim) a2 += wi * (double)(sigma * z[2]);
+        }
+    }
+    gsum[j4] = (float)a0;
+    if (j4 + 1 < dim) gsum[j4 + 1] = (float)a1;
+    if (j4 + 2 < dim) gsum[j4 + 2] = (float)a2;
+    if (j4 + 3 < dim) gsum[j4 + 3] = (float)a3;
+}
+
+// one Adam step; partial sums of step^2 and theta_old^2 per block for the update ratio
+__global__ __launch_bounds__(256) void nicnes_adam_kernel(AdamParams p) {
+    __shared__ double red[2][256];
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double s2 = 0.0, t2 = 0.0;
+    if (j < p.dim) {
+        const float g = p.gsum[j] / p.two_f;                 // gradient_est /= ranked_fitnesses.size (fp32)
+        const double th = p.theta64[j];
+        double m, v;
+        if (p.theta_is_fp32) {
+            // Before the first update theta (and so reg and g') are fp32 arrays, and numpy keeps
+            // python_float * fp32_array in fp32: (1 - b1) * g' and (1 - b2) * (g' * g') are fp32
+            // products added to the fp64 moments (optimizers.py:81-82 with NEP-50 promotion).
+            const float th32 = (float)th;
+            const float reg = p.l2coeff32 * th32;
+            const float gp = -g + reg;
+            const float t1 = p.one_minus_beta1_32 * gp;
+            const float t2 = p.one_minus_beta2_32 * (gp * gp);
+            m = p.beta1 * p.m[j] + (double)t1;
+            v = p.beta2 * p.v[j] + (double)t2;
+        } else {
+            const double reg = p.l2coeff * th;
+            const double gp = (double)(-g) + reg;
+            m = p.beta1 * p.m[j] + p.one_minus_beta1 * gp;
+            v = p.beta2 * p.v[j] + p.one_minus_beta2 * (gp * gp);
+        }
+        const double step = (-p.a * m) / (sqrt(v) + p.epsilon);
+        const double nt = th + step;
+        p.m[j] = m;
+        p.v[j] = v;
+        p.theta64[j] = nt;
+        p.theta32[j] = (float)nt;
+        s2 = step * step;
+        t2 = th * th;
+    }
+    red[0][threadIdx.x] = s2;
+    red[1][threadIdx.x] = t2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + o];
+            red[1][threadIdx.x] += red[1][threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        p.partials[2 * blockIdx.x] = red[0][0];
+        p.partials[2 * blockIdx.x + 1] = red[1][0];
+    }
+}
+
+// fixed-order sum of the per-block partials -> out[0] = |step|^2, out[1] = |theta_old|^2
+__global__ __launch_bounds__(256) void nicnes_sum_partials_kernel(const double* partials, int nblocks, double* out) {
+    __shared__ double red[2][256];
+    double a = 0.0, b = 0.0;
+    for (int i = threadIdx.x; i < nblocks; i += 256) {
+        a += partials[2 * i];
+        b += partials[2 * i + 1];
+    }
+    red[0][threadIdx.x] = a;
+    red[1][threadIdx.x] = b;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + o];
+            red[1][threadIdx.x] += red[1][threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = red[0][0];
+        out[1] = red[1][0];
+    }
+}
+
+extern "C" hipError_t nicnes_launch_noise_index(uint64_t seed, uint64_t iteration, uint64_t member0, int count,
+                                                uint64_t table_len, uint64_t dim, uint64_t* out, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(nicnes_noise_index_kernel, dim3((count + 255) / 256), dim3(256), 0, s, seed, iteration, member0,
+                       count, table_len, dim, out);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, double* cr_out, float* w_out, hipStream_t s) {
+    const size_t lds = (size_t)2 * n * sizeof(double);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)nicnes_rank_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(nicnes_rank_kernel, dim3(1), dim3(1024), lds, s, fit, n, cr_out, w_out);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t nicnes_launch_grad(const float* noise, const uint64_t* idx, const float* w, int count, float sigma,
+                                         int64_t dim, float* gsum, hipStream_t s) {
+    const int64_t n4 = (dim + 3) / 4;
+    hipLaunchKernelGGL(nicnes_grad_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, noise, idx, w, count,
+                       sigma, dim, gsum);
+    return hipGetLastError();
+}
+
+extern "C" int nicnes_adam_blocks(int64_t dim) { return (int)((dim + 255) / 256); }
+
+extern "C" hipError_t nicnes_launch_adam(const AdamParams* p, double* norms_out, hipStream_t s) {
+    const int nb = nicnes_adam_blocks(p->dim);
+    hipLaunchKernelGGL(nicnes_adam_kernel, dim3(nb), dim3(256), 0, s, *p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(nicnes_sum_partials_kernel, dim3(1), dim3(256), 0, s, p->partials, nb, norms_out);
+    return hipGetLastError();
+}

@@ -1,0 +1,78 @@
+"""ctypes binding of libnicnes.so (include/nicnes.h). No fallback: a missing library is an error."""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libnicnes.so')
+
+OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_HIP, ERR_NOMEM = 0, 1, 2, 3, 4
+_NAMES = {ERR_INVALID: 'invalid argument', ERR_UNSUPPORTED: 'not supported', ERR_HIP: 'HIP error',
+          ERR_NOMEM: 'out of device memory'}
+
+# every symbol include/nicnes.h declares (checked by tests/test_abi.py)
+EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicnes_destroy', 'nicnes_last_error',
+           'nicnes_set_noise_table', 'nicnes_set_theta', 'nicnes_get_theta', 'nicnes_set_adam_state',
+           'nicnes_get_adam_state', 'nicnes_set_batch', 'nicnes_set_df_table', 'nicnes_noise_indices',
+           'nicnes_evaluate', 'nicnes_rank_weights', 'nicnes_grad_partial', 'nicnes_adam_step', 'nicnes_stats']
+
+
+class NicnesConfig(ctypes.Structure):
+    _fields_ = [('vocab_size', ctypes.c_int32), ('input_encoding_size', ctypes.c_int32),
+                ('rnn_size', ctypes.c_int32), ('fc_feat_size', ctypes.c_int32), ('seq_length', ctypes.c_int32),
+                ('max_batch', ctypes.c_int32), ('max_refs', ctypes.c_int32), ('max_members', ctypes.c_int32),
+                ('noise_len', ctypes.c_uint64), ('noise_seed', ctypes.c_uint64)]
+
+
+class NicnesError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load the in-tree engine library (built by `make -C nes-img-captioning_amd`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NicnesError('libnicnes.so not built: run `make -C nes-img-captioning_amd` '
+                          '(or __graft_entry__.build()); there is no CPU fallback')
+    L = ctypes.CDLL(LIB_PATH)
+    c = ctypes
+    vp, i32, i64, u64, f32, f64 = c.c_void_p, c.c_int32, c.c_int64, c.c_uint64, c.c_float, c.c_double
+    sig = {
+        'nicnes_param_count': (i64, [vp]),
+        'nicnes_param_offsets': (c.c_int, [vp, vp]),
+        'nicnes_create': (c.c_int, [vp, c.c_int, c.POINTER(vp)]),
+        'nicnes_destroy': (c.c_int, [vp]),
+        'nicnes_last_error': (c.c_char_p, [vp]),
+        'nicnes_set_noise_table': (c.c_int, [vp, vp, u64]),
+        'nicnes_set_theta': (c.c_int, [vp, vp, c.c_int, vp]),
+        'nicnes_get_theta': (c.c_int, [vp, vp, vp, vp]),
+        'nicnes_set_adam_state': (c.c_int, [vp, vp, vp, i64, vp]),
+        'nicnes_get_adam_state': (c.c_int, [vp, vp, vp, vp, vp]),
+        'nicnes_set_batch': (c.c_int, [vp, vp, i32, vp, i32, vp, vp]),
+        'nicnes_set_df_table': (c.c_int, [vp, vp, vp, i64, f64]),
+        'nicnes_noise_indices': (c.c_int, [vp, u64, i32, i32, vp, vp]),
+        'nicnes_evaluate': (c.c_int, [vp, u64, i32, i32, f32, vp, vp, vp]),
+        'nicnes_rank_weights': (c.c_int, [vp, vp, i32, vp, vp, vp]),
+        'nicnes_grad_partial': (c.c_int, [vp, u64, i32, i32, vp, f32, vp, vp]),
+        'nicnes_adam_step': (c.c_int, [vp, vp, i32, f64, f64, f64, f64, f64, vp, vp]),
+        'nicnes_stats': (c.c_int, [vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc, handle=None, what=''):
+    if rc != OK:
+        msg = ''
+        if handle:
+            raw = lib().nicnes_last_error(handle)
+            msg = raw.decode() if raw else ''
+        raise NicnesError('%s failed: %s%s' % (what, _NAMES.get(rc, 'error %d' % rc), (': ' + msg) if msg else ''))

@@ -1,0 +1,196 @@
+"""Engine: a Python owner of one libnicnes handle on one GPU.
+
+PyTorch-ROCm tensors are used for device storage only (their data_ptr() goes through the C ABI);
+all arithmetic of the path runs in the HIP kernels of libnicnes.so.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import NicnesConfig, check
+
+SEQ_LENGTH = 16          # FCModel.seq_length, /root/reference/src/captioning/nets.py:147
+
+
+def pack_ngram(tokens):
+    """Exact uint64 key of an n-gram of token ids (n<<56 | t0<<42 | t1<<28 | t2<<14 | t3); the
+    word strings of array_to_str (/root/reference/src/algorithm/tools/utils.py:34-40) are the ids."""
+    n = len(tokens)
+    assert 1 <= n <= 4
+    key = n << 56
+    for k, t in enumerate(tokens):
+        t = int(t)
+        assert 0 <= t < 16384
+        key |= t << (42 - 14 * k)
+    return key
+
+
+def df_table_arrays(document_frequency):
+    """{tuple-of-str-or-int n-gram: df} -> (sorted uint64 keys, float64 df)."""
+    items = sorted((pack_ngram(tuple(int(w) for w in g)), float(v)) for g, v in document_frequency.items())
+    keys = np.array([k for k, _ in items], dtype=np.uint64)
+    vals = np.array([v for _, v in items], dtype=np.float64)
+    return keys, vals
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+class Engine:
+    """One handle = one GPU. ``device`` is the local cuda index."""
+
+    def __init__(self, vocab_size=9487, input_encoding_size=128, rnn_size=128, fc_feat_size=2048,
+                 seq_length=SEQ_LENGTH, max_batch=128, max_refs=None, max_members=512, noise_len=1 << 27,
+                 noise_seed=0, device=0):
+        self.L = _lib.lib()
+        self.device = torch.device('cuda', device)
+        self.cfg = NicnesConfig(vocab_size, input_encoding_size, rnn_size, fc_feat_size, seq_length, max_batch,
+                                max_refs or 8 * max_batch, max_members, noise_len, noise_seed)
+        self.D = int(self.L.nicnes_param_count(ctypes.byref(self.cfg)))
+        off = (ctypes.c_int64 * 10)()
+        check(self.L.nicnes_param_offsets(ctypes.byref(self.cfg), off), None, 'nicnes_param_offsets')
+        self.offsets = list(off)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_create(ctypes.byref(self.cfg), device, ctypes.byref(h)), None, 'nicnes_create')
+        self.h = h
+        self._keep = {}
+        self.B = 0
+
+    # -------------------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, 'h', None):
+            self.L.nicnes_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _dev(self, a, dtype):
+        if isinstance(a, torch.Tensor):
+            return a.to(device=self.device, dtype=dtype).contiguous()
+        return torch.from_numpy(np.ascontiguousarray(a)).to(device=self.device, dtype=dtype)
+
+    # ---------------------------------------------------------------- state -------------
+    def set_noise_table(self, table):
+        t = self._dev(table, torch.float32)
+        assert t.numel() == self.cfg.noise_len
+        self._keep['noise'] = t
+        check(self.L.nicnes_set_noise_table(self.h, _ptr(t), ctypes.c_uint64(t.numel())), self.h, 'set_noise_table')
+
+    def set_theta(self, theta, fp32_origin=None):
+        """theta: fp32 (reference start, fp32 first-step semantics) or fp64 vector [D]."""
+        if fp32_origin is None:
+            fp32_origin = (theta.dtype == np.float32) if isinstance(theta, np.ndarray) else theta.dtype == torch.float32
+        t = self._dev(theta, torch.float64)
+        assert t.numel() == self.D
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_set_theta(self.h, _ptr(t), int(bool(fp32_origin)), self._stream()), self.h, 'set_theta')
+        self._keep['theta_in'] = t
+
+    def theta(self):
+        t64 = torch.empty(self.D, dtype=torch.float64, device=self.device)
+        t32 = torch.empty(self.D, dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_get_theta(self.h, _ptr(t64), _ptr(t32), self._stream()), self.h, 'get_theta')
+        return t64, t32
+
+    def adam_state(self):
+        m = torch.empty(self.D, dtype=torch.float64, device=self.device)
+        v = torch.empty(self.D, dtype=torch.float64, device=self.device)
+        t = ctypes.c_int64()
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_get_adam_state(self.h, _ptr(m), _ptr(v), ctypes.byref(t), self._stream()), self.h,
+                  'get_adam_state')
+        return m, v, t.value
+
+    def set_adam_state(self, m, v, t):
+        m = self._dev(m, torch.float64)
+        v = self._dev(v, torch.float64)
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_set_adam_state(self.h, _ptr(m), _ptr(v), int(t), self._stream()), self.h,
+                  'set_adam_state')
+        self._keep['adam_m'], self._keep['adam_v'] = m, v
+
+    def set_df_table(self, keys, df, ref_len_log):
+        k = self._dev(np.asarray(keys, np.uint64).view(np.int64), torch.int64)
+        d = self._dev(np.asarray(df, np.float64), torch.float64)
+        self._keep['df_keys'], self._keep['df_vals'] = k, d
+        check(self.L.nicnes_set_df_table(self.h, _ptr(k), _ptr(d), int(k.numel()), float(ref_len_log)), self.h,
+              'set_df_table')
+
+    def set_batch(self, fc, gts):
+        """fc [B, F] fp32 of unique images; gts: per image an int array [n_i, seq_length] of
+        zero-padded label rows (data['gts'], /root/reference/src/captioning/dataloader.py:162)."""
+        fc_t = self._dev(fc, torch.float32)
+        B = fc_t.shape[0]
+        rows, start = [], [0]
+        for g in gts:
+            g = np.asarray(g, np.int32).reshape(-1, self.cfg.seq_length)
+            rows.append(g)
+            start.append(start[-1] + g.shape[0])
+        refs = self._dev(np.concatenate(rows, 0), torch.int32)
+        starts = self._dev(np.array(start, np.int32), torch.int32)
+        self._keep['fc'], self._keep['refs'], self._keep['ref_start'] = fc_t, refs, starts
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_set_batch(self.h, _ptr(fc_t), B, _ptr(refs), int(refs.shape[0]), _ptr(starts),
+                                          self._stream()), self.h, 'set_batch')
+        self.B = B
+
+    # ---------------------------------------------------------------- the hot path -------
+    def noise_indices(self, iteration, member_begin, count):
+        out = torch.empty(count, dtype=torch.int64, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_noise_indices(self.h, ctypes.c_uint64(iteration), member_begin, count, _ptr(out),
+                                              self._stream()), self.h, 'noise_indices')
+        return out
+
+    def evaluate(self, iteration, member_begin, count, sigma, fitness_out=None, return_seq=False):
+        """Fitness (f+, f-) of members [member_begin, +count): tensor [count, 2] fp64 on the GPU."""
+        fit = fitness_out if fitness_out is not None else torch.empty((count, 2), dtype=torch.float64,
+                                                                      device=self.device)
+        seq = torch.empty((count, 2, self.B, self.cfg.seq_length), dtype=torch.int32,
+                          device=self.device) if return_seq else None
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_evaluate(self.h, ctypes.c_uint64(iteration), member_begin, count,
+                                         ctypes.c_float(sigma), _ptr(fit), _ptr(seq), self._stream()), self.h,
+                  'evaluate')
+        return (fit, seq) if return_seq else fit
+
+    def rank_weights(self, fitness_all):
+        """fitness [P, 2] fp64 (whole population) -> (centred ranks [P, 2] fp64, weights [P] fp32)."""
+        P = fitness_all.shape[0]
+        cr = torch.empty((P, 2), dtype=torch.float64, device=self.device)
+        w = torch.empty(P, dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_rank_weights(self.h, _ptr(fitness_all), P, _ptr(cr), _ptr(w), self._stream()), self.h,
+                  'rank_weights')
+        return cr, w
+
+    def grad_partial(self, iteration, member_begin, count, w_shard, sigma, out=None):
+        g = out if out is not None else torch.empty(self.D, dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_grad_partial(self.h, ctypes.c_uint64(iteration), member_begin, count, _ptr(w_shard),
+                                             ctypes.c_float(sigma), _ptr(g), self._stream()), self.h, 'grad_partial')
+        return g
+
+    def adam_step(self, gsum, P, l2coeff, stepsize, beta1=0.9, beta2=0.999, epsilon=1e-08):
+        ratio = ctypes.c_double()
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_adam_step(self.h, _ptr(gsum), P, l2coeff, stepsize, beta1, beta2, epsilon,
+                                          ctypes.byref(ratio), self._stream()), self.h, 'adam_step')
+        return ratio.value
+
+    def stats(self):
+        out = (ctypes.c_int64 * 4)()
+        check(self.L.nicnes_stats(self.h, out), self.h, 'stats')
+        return {'tie_fallbacks': out[0]}

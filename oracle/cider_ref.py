@@ -56,7 +56,9 @@ class CiderDOracle:
     def __init__(self, document_frequency, ref_len_raw, n=4, sigma=6.0):
         self.n = n
         self.sigma = sigma
-        self.document_frequency = defaultdict(float, document_frequency)
+        # n-grams are tuples of word strings; accept integer-id tuples too
+        self.document_frequency = defaultdict(
+            float, {tuple(str(w) for w in g): float(v) for g, v in document_frequency.items()})
         self.ref_len = np.log(float(ref_len_raw))
 
     def counts2vec(self, cnts):

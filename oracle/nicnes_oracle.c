@@ -78,7 +78,16 @@ static float* transpose_perm(const float* W, int rows, int K, int half_order) {
     return WT;
 }
 
-/* acc[r] = fmaf-chain over chain positions; x[k] read through the permutation */
+/* acc[r] continues its fmaf chain over the chain positions; x[k] read through the permutation */
+static void gemv_chain_acc(const float* WT, const float* x, int rows, int K, int half_order, float* acc) {
+    for (int p = 0; p < K; ++p) {
+        const float xv = x[perm_pos(p, K, half_order)];
+        const float* w = WT + (size_t)p * rows;
+        for (int r = 0; r < rows; ++r) acc[r] = fmaf(w[r], xv, acc[r]);
+    }
+}
+
+/* acc[r] = fmaf-chain over chain positions started from the bias */
 static void gemv_chain(const float* WT, const float* bias, const float* x, int rows, int K,
                        int half_order, float* acc) {
     for (int r = 0; r < rows; ++r) acc[r] = bias[r];
@@ -153,13 +162,14 @@ int od_decode(const od_dims* d, const float* theta, const float* fc, int B,
         for (int t = 0; t <= T; ++t) {
             if (t == 0) gemv_chain(WimgT, theta + L.img_b, fc + (size_t)b * F, E, F, half_order, x);
             else memcpy(x, theta + L.emb_w + (size_t)it * E, sizeof(float) * (size_t)E);
+            /* gate sums: one chain per gate, ((b_i2h + Wi.x) + b_h2h) + Wh.h (i2h then h2h, the
+             * order LSTMCore adds them, nets.py:109-111); h = 0 at t = 0 contributes nothing */
             gemv_chain(WiT, theta + L.i2h_b, x, G, E, half_order, si);
-            if (t == 0) memcpy(sh, theta + L.h2h_b, sizeof(float) * (size_t)G);  /* h = 0 */
-            else gemv_chain(WhT, theta + L.h2h_b, h, G, R, half_order, sh);
+            for (int u = 0; u < G; ++u) sh[u] = si[u] + theta[L.h2h_b + u];
+            if (t > 0) gemv_chain_acc(WhT, h, G, R, half_order, sh);
             for (int u = 0; u < R; ++u) {
                 float cn, hn;
-                nn_lstm_cell(si[u] + sh[u], si[R + u] + sh[R + u], si[2 * R + u] + sh[2 * R + u],
-                             si[3 * R + u] + sh[3 * R + u], si[4 * R + u] + sh[4 * R + u], c[u], &cn, &hn);
+                nn_lstm_cell(sh[u], sh[R + u], sh[2 * R + u], sh[3 * R + u], sh[4 * R + u], c[u], &cn, &hn);
                 c[u] = cn;
                 h[u] = hn;
             }
