@@ -1,0 +1,165 @@
+#!/usr/bin/env python3
+"""Benchmark: NIC-NES population members evaluated per second (fc_caption), BASELINE.json's metric.
+
+One step = one full NES iteration over the population on synthetic inputs resident in HBM:
+perturb (in LDS) + greedy decode of both antithetic candidates of every member + CIDEr-D fitness,
+fitness all-gather, centred ranks, weighted noise sum, gradient all-reduce, Adam.
+Workload (BASELINE.json configs[2], 'mscoco_nes.json fc_caption, pop=512 antithetic,
+batch_size=128'): 512 members per GPU, 128 unique images, sigma 0.01, l2coeff 1e-7, Adam 1e-3.
+Multi-GPU is weak scaling: each rank evaluates its own 512 members of a population of 512*N
+(configs[3]'s pop=2048 on 8 GPUs has 256 per GPU; --pop-per-gpu 256 runs that).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'nes-img-captioning_amd'))
+
+METRIC = 'population-members evaluated/sec (fc_caption, pop=512) at 1/2/4/8 GPUs'
+FP32_MFMA_PEAK_TFLOPS = 157.3       # MI355X dense fp32 MFMA (MI355X_MICROARCH.md, chip table)
+HBM_PEAK_GBS = 8000.0
+
+
+def decode_flops_per_member(B, V1=9488, E=128, R=128, F=2048):
+    """Algorithmic FLOPs of one member (2 decodes of B unique rows): img_embed once, 17 cell
+    steps, 16 logit steps per row."""
+    per_row = 2 * (F * E + 17 * (2 * E * 5 * R) + 16 * (R * V1))
+    return 2 * B * per_row
+
+
+def cpu_baseline(args, B):
+    """The reference CPU worker path (torch-CPU restatement, oracle/ref_worker.py) on this box's
+    host cores: one single-threaded process per core, one member per process."""
+    from oracle import ref_worker
+    import nicnes.synthetic as S
+    import torch
+    dims = S.Dims()
+    theta = S.init_theta(dims, 0)
+    fc = S.fc_feats(B, dims.F, 1234, args.bu)
+    m = ref_worker.FCModelRef()
+    torch.nn.utils.vector_to_parameters(torch.from_numpy(theta), m.parameters())
+    with torch.no_grad():
+        base, _ = m.sample(torch.from_numpy(fc))
+    gts, df, ref_len_raw = S.build_references(base.numpy(), dims.vocab_size, 4321, 5, 4096, dims.T)
+    cores = max(1, min(args.cpu_cores, os.cpu_count() or 1))
+    table = S.noise_table(1 << 24, 123)
+    rng = np.random.default_rng(0)
+    n_members = cores * args.cpu_members_per_core
+    deltas = [np.float32(args.sigma) * table[o: o + dims.D]
+              for o in (64 * rng.integers(0, (table.size - dims.D) // 64, n_members))]
+    rate, _, secs = ref_worker.time_members(theta, fc, gts, df, ref_len_raw, deltas, cores)
+    return {'value': round(rate, 4), 'unit': 'members/s', 'cores': cores, 'kind': 'port',
+            'sample': '%d members (2 rollouts of %d rows = %d unique images x5, 18+18 steps, pure-Python '
+                      'CIDEr-D), one single-threaded torch process per core; mean %.2f s/member'
+                      % (n_members, 5 * B, B, float(secs.mean()))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--pop-per-gpu', type=int, default=512)
+    ap.add_argument('--batch', type=int, default=128)
+    ap.add_argument('--sigma', type=float, default=0.01)
+    ap.add_argument('--noise-len', type=int, default=1 << 27)
+    ap.add_argument('--bu', action='store_true', help="'bu' features: ReLU(N(0,1)) fc (configs[4])")
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-cores', type=int, default=16)
+    ap.add_argument('--cpu-members-per-core', type=int, default=1)
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    B = args.batch
+
+    # CPU leg first, before this process touches the GPU (its pool forks)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, B)
+
+    import torch
+    import torch.distributed as dist
+    import nicnes
+    import nicnes.synthetic as S
+    from nicnes.population import PopulationRunner
+
+    torch.cuda.set_device(local_rank)
+    group = None
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+    P_local = args.pop_per_gpu
+    P = P_local * world
+    eng = nicnes.Engine(max_batch=B, max_members=P_local, noise_len=args.noise_len, noise_seed=0,
+                        device=local_rank)
+    S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu)
+    runner = PopulationRunner(eng, P, args.sigma, l2coeff=1e-7, stepsize=1e-3, rank=rank, world_size=world,
+                              group=group)
+    it = 1
+    for _ in range(args.warmup):
+        runner.step(it)
+        it += 1
+    eng.set_timing(True)
+    dec_ms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        runner.step(it)                      # adam_step synchronises on its ratio readback
+        dec_ms.append(eng.kernel_times()[0])
+        it += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    value = P * args.steps / dt
+    dec_s = float(np.mean(dec_ms)) / 1e3
+    flops = decode_flops_per_member(B) * P_local
+    achieved = flops / dec_s / 1e12
+    traffic = None
+    pmc = os.path.join(REPO, 'profiles', 'r01_decode_pmc.json')
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get('hbm_bytes_per_launch')
+    out = {
+        'metric': METRIC, 'value': round(value, 3), 'unit': 'members/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+        'data': 'synthetic (seeded fc features, xavier-init fc_caption theta, substituted refs, 2^27 noise table)',
+        'config': {'workload': 'mscoco_nes.json fc_caption, pop=%d antithetic (%d/GPU), batch_size=%d unique '
+                               'images, sigma %.3g, full iteration (decode+CIDEr-D+ranks+noise sum+Adam)'
+                               % (P, P_local, B, args.sigma) + (", 'bu' fc features" if args.bu else ''),
+                   'population': P, 'members_per_gpu': P_local, 'batch_size': B, 'seq_length': 16,
+                   'vocab_size': 9487, 'parallelism': 'population-sharded x%d, RCCL all-gather + all-reduce'
+                   % world},
+        'roofline': {'bound': 'mfma', 'kernel': 'nicnes_decode_kernel', 'achieved': round(achieved, 3),
+                     'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                     'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,
+                     'decode_ms_per_launch': round(dec_s * 1e3, 3),
+                     'algorithmic_flop_per_launch': flops},
+        'cpu_baseline': cpu,
+        'tie_fallbacks': eng.stats()['tie_fallbacks'],
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

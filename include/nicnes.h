@@ -111,6 +111,12 @@ int nicnes_adam_step(nicnes_handle* h, const float* gsum, int32_t P, double l2co
 /* diagnostics: [0] = exact-pass fallbacks of the greedy tie rule since creation (synchronising) */
 int nicnes_stats(nicnes_handle* h, int64_t* out4_host);
 
+/* Kernel timing with HIP events recorded on the launch stream around the decode and CIDEr-D
+ * launches of nicnes_evaluate (off by default). nicnes_kernel_times synchronises on the events
+ * and returns the last call's [0] = decode ms, [1] = CIDEr-D ms. */
+int nicnes_set_timing(nicnes_handle* h, int on);
+int nicnes_kernel_times(nicnes_handle* h, float* out2_host);
+
 #ifdef __cplusplus
 }
 #endif

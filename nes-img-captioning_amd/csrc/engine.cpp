@@ -58,6 +58,9 @@ struct nicnes_handle {
     int32_t* stats = nullptr;
     double* partials = nullptr;
     double* norms = nullptr;
+
+    bool timing = false;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -190,6 +193,8 @@ int nicnes_destroy(nicnes_handle* h) {
                     h->ref_norm, h->nidx, h->seq, h->dscratch, h->stats, h->partials, h->norms};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
+    for (hipEvent_t e : h->ev)
+        if (e) (void)hipEventDestroy(e);
     delete h;
     return NICNES_OK;
 }
@@ -337,9 +342,12 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
     p.off_h2h_b = h->off[8];
     // rows a member never writes (all finished early) must read as 0 (nets.py:188 zeros)
     HIPC(h, hipMemsetAsync(p.seq, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(int32_t), s));
+    if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
     HIPC(h, nicnes_launch_decode(&p, count, nslabs_of(h->B), s));
+    if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     CiderTables tb = tables_of(h);
     HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, fitness_out, s));
+    if (h->timing) HIPC(h, hipEventRecord(h->ev[2], s));
     return NICNES_OK;
 }
 
@@ -409,6 +417,24 @@ int nicnes_stats(nicnes_handle* h, int64_t* out4_host) {
     HIPC(h, hipSetDevice(h->device));
     HIPC(h, hipMemcpy(st, h->stats, sizeof st, hipMemcpyDeviceToHost));
     for (int i = 0; i < 4; ++i) out4_host[i] = st[i];
+    return NICNES_OK;
+}
+
+int nicnes_set_timing(nicnes_handle* h, int on) {
+    if (!h) return NICNES_ERR_INVALID;
+    HIPC(h, hipSetDevice(h->device));
+    if (on && !h->ev[0])
+        for (auto& e : h->ev) HIPC(h, hipEventCreate(&e));
+    h->timing = on != 0;
+    return NICNES_OK;
+}
+
+int nicnes_kernel_times(nicnes_handle* h, float* out2_host) {
+    if (!h || !out2_host || !h->ev[0]) return NICNES_ERR_INVALID;
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, hipEventSynchronize(h->ev[2]));
+    HIPC(h, hipEventElapsedTime(&out2_host[0], h->ev[0], h->ev[1]));
+    HIPC(h, hipEventElapsedTime(&out2_host[1], h->ev[1], h->ev[2]));
     return NICNES_OK;
 }
 

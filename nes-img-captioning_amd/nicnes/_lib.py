@@ -13,7 +13,8 @@ _NAMES = {ERR_INVALID: 'invalid argument', ERR_UNSUPPORTED: 'not supported', ERR
 EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicnes_destroy', 'nicnes_last_error',
            'nicnes_set_noise_table', 'nicnes_set_theta', 'nicnes_get_theta', 'nicnes_set_adam_state',
            'nicnes_get_adam_state', 'nicnes_set_batch', 'nicnes_set_df_table', 'nicnes_noise_indices',
-           'nicnes_evaluate', 'nicnes_rank_weights', 'nicnes_grad_partial', 'nicnes_adam_step', 'nicnes_stats']
+           'nicnes_evaluate', 'nicnes_rank_weights', 'nicnes_grad_partial', 'nicnes_adam_step', 'nicnes_stats',
+           'nicnes_set_timing', 'nicnes_kernel_times']
 
 
 class NicnesConfig(ctypes.Structure):
@@ -60,6 +61,8 @@ def lib():
         'nicnes_grad_partial': (c.c_int, [vp, u64, i32, i32, vp, f32, vp, vp]),
         'nicnes_adam_step': (c.c_int, [vp, vp, i32, f64, f64, f64, f64, f64, vp, vp]),
         'nicnes_stats': (c.c_int, [vp, vp]),
+        'nicnes_set_timing': (c.c_int, [vp, c.c_int]),
+        'nicnes_kernel_times': (c.c_int, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -190,6 +190,15 @@ class Engine:
                                           ctypes.byref(ratio), self._stream()), self.h, 'adam_step')
         return ratio.value
 
+    def set_timing(self, on=True):
+        check(self.L.nicnes_set_timing(self.h, int(bool(on))), self.h, 'set_timing')
+
+    def kernel_times(self):
+        """(decode_ms, cider_ms) of the last evaluate() (HIP events on its stream)."""
+        out = (ctypes.c_float * 2)()
+        check(self.L.nicnes_kernel_times(self.h, out), self.h, 'kernel_times')
+        return float(out[0]), float(out[1])
+
     def stats(self):
         out = (ctypes.c_int64 * 4)()
         check(self.L.nicnes_stats(self.h, out), self.h, 'stats')

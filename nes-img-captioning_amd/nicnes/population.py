@@ -1,0 +1,57 @@
+"""One NIC-NES iteration over a population, sharded over the ranks of a torch.distributed group.
+
+Replaces the master/worker split of the reference for the hot path:
+  workers: NESWorker.fitness per member            (/root/reference/src/algorithm/nic_nes/nic_nes_worker.py:115-161)
+  master : gradient_estimate + optimizer.update     (/root/reference/src/algorithm/nic_nes/nic_nes_master.py:123-137)
+with members [r*P/N, (r+1)*P/N) evaluated on rank r. The exchange is one all-gather of the (P, 2)
+fitness (every rank then ranks the whole population identically) and one all-reduce (sum) of the
+D-float weighted noise sum; Adam then runs replicated, so theta needs no broadcast.
+On ROCm the 'nccl' backend is RCCL over xGMI.
+"""
+import torch
+import torch.distributed as dist
+
+
+class PopulationRunner:
+    def __init__(self, engine, population, sigma, l2coeff=0.0, stepsize=1e-3, beta1=0.9, beta2=0.999,
+                 epsilon=1e-08, rank=0, world_size=1, group=None):
+        assert population % world_size == 0, 'population must split evenly over ranks'
+        self.e = engine
+        self.P = population
+        self.sigma = float(sigma)
+        self.l2coeff, self.stepsize, self.beta1, self.beta2, self.epsilon = l2coeff, stepsize, beta1, beta2, epsilon
+        self.rank, self.world = rank, world_size
+        self.group = group
+        self.local = population // world_size
+        self.m0 = rank * self.local
+        dev = engine.device
+        self.fit_local = torch.empty((self.local, 2), dtype=torch.float64, device=dev)
+        self.fit_all = torch.empty((self.P, 2), dtype=torch.float64, device=dev) if world_size > 1 else self.fit_local
+        self.gsum = torch.empty(engine.D, dtype=torch.float32, device=dev)
+
+    def evaluate(self, iteration):
+        """this rank's members -> fitness [local, 2] (f+, f-)"""
+        self.e.evaluate(iteration, self.m0, self.local, self.sigma, fitness_out=self.fit_local)
+        return self.fit_local
+
+    def exchange_fitness(self):
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.fit_all, self.fit_local, group=self.group)
+        return self.fit_all
+
+    def update(self, iteration):
+        """ranks -> weighted noise sum (local members) -> all-reduce -> Adam. Returns the update ratio."""
+        _, w = self.e.rank_weights(self.fit_all)
+        self.e.grad_partial(iteration, self.m0, self.local, w[self.m0:self.m0 + self.local], self.sigma,
+                            out=self.gsum)
+        if self.world > 1:
+            dist.all_reduce(self.gsum, op=dist.ReduceOp.SUM, group=self.group)
+        return self.e.adam_step(self.gsum, self.P, self.l2coeff, self.stepsize, self.beta1, self.beta2,
+                                self.epsilon)
+
+    def step(self, iteration):
+        """One full NES iteration. Returns (fitness [P, 2] on device, update ratio)."""
+        self.evaluate(iteration)
+        self.exchange_fitness()
+        ratio = self.update(iteration)
+        return self.fit_all, ratio
