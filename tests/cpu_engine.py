@@ -1,0 +1,65 @@
+"""Test helper: an Engine look-alike on CPU tensors built from the oracle (test infrastructure only),
+so the sharded PopulationRunner logic (nicnes/population.py) can run over gloo without a GPU."""
+import numpy as np
+import torch
+
+from oracle import cider_ref as CR
+from oracle import oracle as O
+
+
+class OracleEngine:
+    def __init__(self, dims, theta32, fc, gts, df, ref_len_raw, table, noise_seed=0):
+        self.device = torch.device('cpu')
+        self.dims, self.D = dims, dims.D
+        self.fc, self.gts, self.table, self.seed = fc, gts, table, noise_seed
+        self.scorer = CR.CiderDOracle(df, ref_len_raw)
+        self.adam = None
+        self.theta32 = theta32.copy()
+        self.theta_src = theta32.copy()
+
+    def _idx(self, iteration, m):
+        return O.noise_index(self.seed, iteration, m, self.table.size, self.D)
+
+    def evaluate(self, iteration, member_begin, count, sigma, fitness_out=None):
+        out = fitness_out if fitness_out is not None else torch.empty((count, 2), dtype=torch.float64)
+        for k in range(count):
+            idx = self._idx(iteration, member_begin + k)
+            for s, sign in enumerate((+1, -1)):
+                seq, _, _ = O.decode(self.dims, O.perturb(self.theta32, self.table, idx, sigma, sign), self.fc)
+                out[k, s] = CR.rollout_fitness(self.scorer, seq, self.gts)[0]
+        return out
+
+    def rank_weights(self, fitness_all):
+        w, cr = O.weights_from_fitness(fitness_all.numpy())
+        return torch.from_numpy(cr), torch.from_numpy(w)
+
+    def grad_partial(self, iteration, member_begin, count, w_shard, sigma, out=None):
+        acc = np.zeros(self.D, np.float64)
+        s = np.float32(sigma)
+        for k in range(count):
+            idx = self._idx(iteration, member_begin + k)
+            acc += np.float64(w_shard[k].item()) * (s * self.table[idx: idx + self.D]).astype(np.float64)
+        g = torch.from_numpy(acc.astype(np.float32))
+        if out is not None:
+            out.copy_(g)
+            return out
+        return g
+
+    def adam_step(self, gsum, P, l2coeff, stepsize, beta1=0.9, beta2=0.999, epsilon=1e-08):
+        if self.adam is None:
+            self.adam = O.AdamOracle(self.theta_src.copy(), stepsize, beta1, beta2, epsilon)
+        g = gsum.numpy().astype(np.float32) / np.float32(2 * P)
+        ratio, theta = O.master_update(self.adam, g, l2coeff)
+        self.theta32 = np.asarray(theta).astype(np.float32)
+        return float(ratio)
+
+
+def tiny_workload(B=4, seed=0):
+    import nicnes.synthetic as S
+    dims = O.Dims(vocab_size=63, E=32, R=32, F=64)
+    theta = O.make_theta(dims, seed, 4.0, 0.1)
+    fc = np.random.Generator(np.random.PCG64(1234)).standard_normal((B, dims.F)).astype(np.float32)
+    base, _, _ = O.decode(dims, theta, fc)
+    gts, df, n = S.build_references(base, dims.vocab_size, seed=5, n_refs=5, df_sets=64)
+    table = O.noise_table(1 << 16, 123)
+    return dims, theta, fc, gts, df, n, table
