@@ -33,6 +33,12 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #define STAGE_FLOATS (2 * SIGN_FLOATS + 64)           // W+ | W- | bias+ (32) | bias- (32)
 #define LOG2E 1.44269504088896340736f
 #define NEG_INF (-__builtin_inff())
+#ifndef DECODE_ABLATE
+#define DECODE_ABLATE 0    // timing-only builds (scripts/ablate.py): 1 no logit epilogue, 2 no logit
+#endif                     // staging, 4 no LSTM cell, 8 no logit-loop barrier -- wrong results
+#ifndef DECODE_SCHED
+#define DECODE_SCHED 0
+#endif
 
 // ---- buffer helpers ------------------------------------------------------------------------
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
@@ -69,15 +75,16 @@ __device__ __forceinline__ void stage_load(rsrc_t theta_r, rsrc_t noise_r, const
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         const int f = tid + NTHREADS * u, row = f >> 5, q = f & 31;
-        const int rc = row < d.nvalid ? row : d.nvalid - 1;          // clamp, zero after the load
+        const int rc = row < d.nvalid ? row : max(d.nvalid - 1, 0);  // clamp, zero after the load
         const uint32_t off = 4u * (d.w_off + (uint32_t)((d.row0 + rc) * d.ld + d.k0 + 4 * q));
         const f32x4 w = ld4(theta_r, off), z = ld4(noise_r, off);
         const bool ok = row < d.nvalid;
         s.w[u] = ok ? w : f32x4{0.f, 0.f, 0.f, 0.f};
         s.z[u] = ok ? z : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    if (tid < 32) {
-        const int rc = tid < d.nvalid ? tid : 0;
+    {   // every thread loads bias row (tid & 31): no divergent branch in the staging code
+        const int r = tid & 31;
+        const int rc = r < d.nvalid ? r : 0;
         const uint32_t off = 4u * (d.b_off + (uint32_t)(d.row0 + rc));
         s.bw = ld1(theta_r, off);
         s.bz = ld1(noise_r, off);
@@ -96,11 +103,12 @@ __device__ __forceinline__ void stage_store(float* buf, const TileDesc& d, float
         *reinterpret_cast<f32x4*>(buf + o) = plus;
         *reinterpret_cast<f32x4*>(buf + SIGN_FLOATS + o) = minus;
     }
-    if (tid < 32) {
+    {   // slot (tid & 63): bias+ rows 0..31, bias- rows 32..63; every wave writes the same
+        // values to the same 64 slots (benign, branch-free)
+        const int r = tid & 31;
         const float delta = sigma * s.bz;
-        const bool ok = tid < d.nvalid;
-        buf[2 * SIGN_FLOATS + tid] = ok ? s.bw + delta : d.pad_bias;
-        buf[2 * SIGN_FLOATS + 32 + tid] = ok ? s.bw - delta : d.pad_bias;
+        const float v = (tid & 32) ? s.bw - delta : s.bw + delta;
+        buf[2 * SIGN_FLOATS + (tid & 63)] = r < d.nvalid ? v : d.pad_bias;
     }
 }
 
@@ -132,6 +140,37 @@ __device__ __forceinline__ f32x16 mfma_tile(f32x16 acc, const float* w, const fl
     return acc;
 }
 
+// same product with the A fragments of sub-chunk T+1 read while sub-chunk T's MFMAs run
+__device__ __forceinline__ f32x16 mfma_tile_pf(f32x16 acc, const float* w, const float (&Bop)[64], int lane) {
+    const float* row = w + (lane & 31) * LDS_ROW + (lane >> 5) * 16;
+    f32x4 a[4], an[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a[c] = *reinterpret_cast<const f32x4*>(row + 4 * c);
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+        if (T < 3) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) an[c] = *reinterpret_cast<const f32x4*>(row + (T + 1) * 32 + 4 * c);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[jj >> 2][jj & 3], Bop[16 * T + jj], acc, 0, 0, 0);
+        if (T < 3) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) a[c] = an[c];
+        }
+    }
+#if DECODE_SCHED >= 3
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 1);
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+        if (T < 3) __builtin_amdgcn_sched_group_barrier(0x100, 4, 1);
+        __builtin_amdgcn_sched_group_barrier(0x008, 16, 1);
+    }
+#endif
+    return acc;
+}
+
 // img_embed variant: the B operand (fc row chunk) is read per 32-k sub-chunk from global
 __device__ __forceinline__ f32x16 mfma_tile_fc(f32x16 acc, const float* w, rsrc_t fc_r, uint32_t frow_off, int lane) {
     const float* row = w + (lane & 31) * LDS_ROW + (lane >> 5) * 16;
@@ -160,7 +199,7 @@ struct RowState {
 };
 
 __device__ __forceinline__ void row_state_init(RowState& st) {
-    st.m = NEG_INF; st.s = 0.f;
+    st.m = -1.0e30f; st.s = 0.f;   // finite, and m * log2e stays finite: exp2 args never NaN
     st.r1v = NEG_INF; st.r1i = 0x7fffffff;
     st.r0v = NEG_INF; st.r0i = 0x7fffffff;
     st.ev = NEG_INF;
@@ -174,10 +213,9 @@ __device__ __forceinline__ void logit_epilogue(RowState& st, const f32x16& acc, 
     float tmax = acc[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) tmax = fmaxf(tmax, acc[r]);
-    if (tmax > st.m) {
-        st.s = (st.m == NEG_INF) ? 0.f : st.s * __builtin_amdgcn_exp2f((st.m - tmax) * LOG2E);
-        st.m = tmax;
-    }
+    const float mnew = fmaxf(st.m, tmax);
+    st.s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
+    st.m = mnew;
     float ts = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) ts += __builtin_amdgcn_exp2f((acc[r] - st.m) * LOG2E);
@@ -192,6 +230,192 @@ __device__ __forceinline__ void logit_epilogue(RowState& st, const f32x16& acc, 
         st.r0i = c ? st.r1i : st.r0i;
         st.r1v = c ? L : st.r1v;
         st.r1i = c ? v : st.r1i;
+    }
+}
+
+// One logit tile with a hand-placed schedule: the 64 dependent MFMAs of tile n, and between
+// consecutive MFMAs a slice of (a) the epilogue of tile n-1 and (b) the LDS store of the staged
+// tile n+1. In-order issue puts every slice in the shadow of the MFMA ahead of it (the next
+// dependent MFMA waits for that one anyway); sched_barrier(0) pins the order.
+// Epilogue slots: 0-6 tile max + rescale, 8-23 sum of exp2, 24-39 record updates;
+// staging slots 44-51 (row u=0), 52-59 (u=1), 60 bias.
+__device__ __forceinline__ void epi_slot(int j, RowState& st, const f32x16& P, int vbase, float (&x)[5],
+                                         float& ml) {
+    if (j < 5) {
+        x[j] = fmaxf(fmaxf(P[3 * j], P[3 * j + 1]), P[3 * j + 2]);
+    } else if (j == 5) {
+        x[0] = fmaxf(fmaxf(x[0], x[1]), x[2]);
+    } else if (j == 6) {
+        const float tmax = fmaxf(fmaxf(x[0], x[3]), fmaxf(x[4], P[15]));
+        const float mnew = fmaxf(st.m, tmax);
+        st.s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
+        st.m = mnew;
+        ml = mnew * LOG2E;
+    } else if (j >= 8 && j < 24) {
+        const int r = j - 8;
+        st.s += __builtin_amdgcn_exp2f(__builtin_fmaf(P[r], LOG2E, -ml));
+    } else if (j >= 24 && j < 40) {
+        const int r = j - 24;
+        const float L = P[r];
+        const int v = vbase + (r & 3) + 8 * (r >> 2);
+        const bool c = L > st.r1v;
+        st.ev = c ? st.r0v : st.ev;
+        st.r0v = c ? st.r1v : st.r0v;
+        st.r0i = c ? st.r1i : st.r0i;
+        st.r1v = c ? L : st.r1v;
+        st.r1i = c ? v : st.r1i;
+    }
+}
+
+__device__ __forceinline__ void store_slot(int j, float* buf, const TileDesc& d, float sigma, int tid,
+                                           const StageRegs& s) {
+    if (j >= 44 && j < 60) {
+        const int u = (j - 44) >> 3, part = (j - 44) & 7;
+        const int f = tid + NTHREADS * u, row = f >> 5, q = f & 31;
+        const int o = row * LDS_ROW + (q >> 3) * 32 + (q & 1) * 16 + 4 * ((q & 7) >> 1);
+        if (part == 0) {
+            const f32x4 delta = sigma * s.z[u];
+            *reinterpret_cast<f32x4*>(buf + o) = s.w[u] + delta;
+            *reinterpret_cast<f32x4*>(buf + SIGN_FLOATS + o) = s.w[u] - delta;
+        }
+    } else if (j == 60) {
+        const int r = tid & 31;
+        const float delta = sigma * s.bz;
+        const float v = (tid & 32) ? s.bw - delta : s.bw + delta;
+        buf[2 * SIGN_FLOATS + (tid & 63)] = r < d.nvalid ? v : d.pad_bias;
+    }
+}
+
+__device__ __forceinline__ f32x16 logit_tile_sched(const float* w, const float* bias, const float (&Bop)[64], int lane,
+                                                   RowState& st, const f32x16& prev, int vbase_prev, float* nbuf,
+                                                   const TileDesc& nd, float sigma, int tid, const StageRegs& s) {
+    const int hh = lane >> 5;
+    const float* row = w + (lane & 31) * LDS_ROW + hh * 16;
+    f32x16 acc = bias_init(bias, hh);
+    f32x4 a[4], an[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a[c] = *reinterpret_cast<const f32x4*>(row + 4 * c);
+    float x[5], ml = 0.f;
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+        if (T < 3) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) an[c] = *reinterpret_cast<const f32x4*>(row + (T + 1) * 32 + 4 * c);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            const int j = 16 * T + jj;
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[jj >> 2][jj & 3], Bop[j], acc, 0, 0, 0);
+            epi_slot(j, st, prev, vbase_prev, x, ml);
+            store_slot(j, nbuf, nd, sigma, tid, s);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (T < 3) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) a[c] = an[c];
+        }
+    }
+    return acc;
+}
+
+// ---- 64-row logit stages ---------------------------------------------------------------------
+#define STAGE64_FLOATS (2 * 64 * LDS_ROW + 128)       // W+ (64 rows) | W- | bias+ (64) | bias- (64)
+
+struct Stage64Regs {
+    f32x4 w[4], z[4];
+    float bw, bz;
+};
+
+__device__ __forceinline__ void stage64_load(rsrc_t lw, rsrc_t lz, rsrc_t lbw, rsrc_t lbz, int s, int tid,
+                                             Stage64Regs& r) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int f = tid + NTHREADS * u, row = f >> 5, q = f & 31;
+        const uint32_t off = 4u * (uint32_t)((64 * s + row) * 128 + 4 * q);
+        r.w[u] = ld4(lw, off);
+        r.z[u] = ld4(lz, off);
+    }
+    const uint32_t boff = 4u * (uint32_t)(64 * s + (tid & 63));
+    r.bw = ld1(lbw, boff);
+    r.bz = ld1(lbz, boff);
+}
+
+__device__ __forceinline__ void stage64_store(float* buf, int s, int V1, float sigma, int tid, const Stage64Regs& r) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int f = tid + NTHREADS * u, row = f >> 5, q = f & 31;
+        const int o = row * LDS_ROW + (q >> 3) * 32 + (q & 1) * 16 + 4 * ((q & 7) >> 1);
+        const f32x4 delta = sigma * r.z[u];           // fp32(sigma * z), nets.py:102
+        *reinterpret_cast<f32x4*>(buf + o) = r.w[u] + delta;                    // nets.py:113
+        *reinterpret_cast<f32x4*>(buf + 64 * LDS_ROW + o) = r.w[u] - delta;     // nic_nes_worker.py:151
+    }
+    const int row = tid & 63, sg = (tid >> 6) & 1;     // every pair of waves writes all 128 slots
+    const float delta = sigma * r.bz;
+    const float v = sg ? r.bw - delta : r.bw + delta;
+    buf[2 * 64 * LDS_ROW + 64 * sg + row] = (64 * s + row < V1) ? v : NEG_INF;
+}
+
+// two independent accumulator chains (rows 0-31 and 32-63 of the stage) over the same B
+__device__ __forceinline__ void mfma_stage64(const float* w, const float* bias, const float (&Bop)[64], int lane,
+                                             f32x16& acc0, f32x16& acc1) {
+    const int hh = lane >> 5;
+    const float* row0 = w + (lane & 31) * LDS_ROW + hh * 16;
+    const float* row1 = row0 + 32 * LDS_ROW;
+    acc0 = bias_init(bias, hh);
+    acc1 = bias_init(bias + 32, hh);
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+        f32x4 a0[4], a1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            a0[c] = *reinterpret_cast<const f32x4*>(row0 + T * 32 + 4 * c);
+            a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bop[16 * T + jj], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
+        }
+    }
+}
+
+__device__ __forceinline__ void records16(RowState& st, const f32x16& P, int vbase) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float L = P[r];
+        const int v = vbase + (r & 3) + 8 * (r >> 2);
+        const bool c = L > st.r1v;
+        st.ev = c ? st.r0v : st.ev;
+        st.r0v = c ? st.r1v : st.r0v;
+        st.r0i = c ? st.r1i : st.r0i;
+        st.r1v = c ? L : st.r1v;
+        st.r1i = c ? v : st.r1i;
+    }
+}
+
+// epilogue of one stage: P0 holds vocab vbase + (r&3) + 8(r>>2), P1 the same + 32.
+// Record scans run only in the (wave-uniform) case that some lane sees a new running max.
+__device__ __forceinline__ void epilogue64(RowState& st, const f32x16& P0, const f32x16& P1, int vbase) {
+    float t0 = fmaxf(fmaxf(P0[0], P0[1]), P0[2]);
+    float t1 = fmaxf(fmaxf(P1[0], P1[1]), P1[2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) {
+        t0 = fmaxf(fmaxf(t0, P0[r]), P0[r + 1]);
+        t1 = fmaxf(fmaxf(t1, P1[r]), P1[r + 1]);
+    }
+    const float tmax = fmaxf(fmaxf(t0, P0[15]), fmaxf(t1, P1[15]));
+    const float mnew = fmaxf(st.m, tmax);
+    const float ml = mnew * LOG2E;
+    float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(P0[r], LOG2E, -ml));
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(P1[r], LOG2E, -ml));
+    st.s = s;
+    st.m = mnew;
+    if (__any(tmax > st.r1v)) {
+        records16(st, P0, vbase);
+        records16(st, P1, vbase + 32);
     }
 }
 
@@ -228,6 +452,11 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
     // lane-private spill slots (c | h' | 20 partial gate tiles), [slot][lane] per wave
     float* wscr = p.scratch + ((size_t)(member * gridDim.y + slab) * 8 + wave) * (SCR_SLOTS * 64);
     const rsrc_t scr_r = make_rsrc(wscr, SCR_SLOTS * 64 * 4);
+    // logit weight / bias views bounded to V1 rows: padding rows of the last stage read 0
+    const rsrc_t lw_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
+    const rsrc_t lz_r = make_rsrc(p.noise + nidx + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
+    const rsrc_t lbw_r = make_rsrc(p.theta + p.off_log_b, 4u * (uint32_t)p.V1);
+    const rsrc_t lbz_r = make_rsrc(p.noise + nidx + p.off_log_b, 4u * (uint32_t)p.V1);
     const uint32_t lo = 4u * lane;
 #define C_SLOT(s) (4u * 64u * (uint32_t)(s))
 #define H_SLOT(s) (4u * 64u * (uint32_t)(64 + (s)))
@@ -290,19 +519,19 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
         // ========== LSTM cell (nets.py:98-134) ==============================================
         // gate sum s = ((b_i2h + Wi.x) + b_h2h) + Wh.h : one fma chain per gate (the oracle's
         // definition; i2h then h2h as LSTMCore adds them, nets.py:109-111). Tiles 0..19 run the
-        // i2h products and park the 20 partial gate tiles in lane-private scratch; tiles 20..39
-        // finish them with h2h, so x and h are never live in registers together.
+        // i2h products into 20 lane-private gate-sum slots (slot 5U+q: gate chunk q, units
+        // 32U..32U+31); tiles 20..39 add b_h2h + Wh.h in place, so x and h are never live in
+        // registers together; then nn_lstm_cell (the oracle's own function) runs per unit.
+#if !(DECODE_ABLATE & 4)
         {
             const int ntile = 40;
             auto desc = [&](int n) {
-                const int which = n >= 20, m = n - 20 * which, U = m / 5, qi = m % 5;
-                const int q = qi < 2 ? 3 + qi : qi - 2;        // (3,4,0,1,2): g1, g2, in, forget, out
+                const int which = n >= 20, m = n - 20 * which, U = m / 5, q = m % 5;
                 TileDesc d;
                 d.w_off = (uint32_t)(which ? p.off_h2h_w : p.off_i2h_w); d.ld = 128; d.row0 = q * 128 + 32 * U;
                 d.nvalid = 32; d.k0 = 0; d.b_off = (uint32_t)(which ? p.off_h2h_b : p.off_i2h_b); d.pad_bias = 0.f;
                 return d;
             };
-            float g[16];      // holds max(g1,g2), then i*g, then c'
             stage_load(theta_r, noise_r, desc(0), tid, sr);
             stage_store(lds, desc(0), sigma, tid, sr);
             __syncthreads();
@@ -316,69 +545,102 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
                 stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), sigma, tid, sr);
                 __syncthreads();
             }
-            // pass 2: + b_h2h + Wh.h, then the cell elementwise (x not live)
+            // pass 2: + b_h2h + Wh.h (x not live)
 #pragma unroll
             for (int i = 0; i < 64; ++i) hB[i] = (t == 0) ? 0.f : ld1(scr_r, lo, H_SLOT(i));
             for (int n = 20; n < ntile; ++n) {
-                if (n + 1 < ntile) stage_load(theta_r, noise_r, desc(n + 1), tid, sr);
+                const int nn = min(n + 1, ntile - 1);
+                stage_load(theta_r, noise_r, desc(nn), tid, sr);
                 const float* buf = lds + (n & 1) * STAGE_FLOATS;
-                const int m = n - 20, U = m / 5, qi = m % 5;
-                const f32x16 bias = bias_init(buf + 2 * SIGN_FLOATS + 32 * sgn, hh);
+                const int m = n - 20;
                 f32x16 acc;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = ld1(scr_r, lo, P_SLOT(16 * m + r));
-                acc = acc + bias;
+                acc = acc + bias_init(buf + 2 * SIGN_FLOATS + 32 * sgn, hh);
                 if (t > 0) acc = mfma_tile(acc, buf + sgn * SIGN_FLOATS, hB, lane);   // h = 0 at t = 0
-                if (qi == 0) {                                              // q = 3: g1
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) g[r] = acc[r];
-                } else if (qi == 1) {                                       // q = 4: max(g1, g2)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) g[r] = g[r] > acc[r] ? g[r] : acc[r];
-                } else if (qi == 2) {                                       // q = 0: i*g
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) g[r] = nn_sigmoidf(acc[r]) * g[r];
-                } else if (qi == 3) {                                       // q = 1: c' = f*c + i*g
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const float cold = (t == 0) ? 0.f : ld1(scr_r, lo, C_SLOT(16 * U + r));
-                        const float fc_ = nn_sigmoidf(acc[r]) * cold;
-                        g[r] = fc_ + g[r];
-                        st1(scr_r, lo, C_SLOT(16 * U + r), g[r]);
-                    }
-                } else {                                                    // q = 2: h' = o*tanh(c')
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) st1(scr_r, lo, H_SLOT(16 * U + r), nn_sigmoidf(acc[r]) * nn_tanhf(g[r]));
-                }
-                if (n + 1 < ntile) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), sigma, tid, sr);
+                for (int r = 0; r < 16; ++r) st1(scr_r, lo, P_SLOT(16 * m + r), acc[r]);
+                stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(nn), sigma, tid, sr);
                 __syncthreads();
+            }
+            // elementwise cell: c' = f*c + i*max(g1,g2), h' = o*tanh(c')
+            for (int U = 0; U < 4; ++U) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float s0 = ld1(scr_r, lo, P_SLOT(16 * (5 * U + 0) + r));
+                    const float s1 = ld1(scr_r, lo, P_SLOT(16 * (5 * U + 1) + r));
+                    const float s2 = ld1(scr_r, lo, P_SLOT(16 * (5 * U + 2) + r));
+                    const float s3 = ld1(scr_r, lo, P_SLOT(16 * (5 * U + 3) + r));
+                    const float s4 = ld1(scr_r, lo, P_SLOT(16 * (5 * U + 4) + r));
+                    const float cold = (t == 0) ? 0.f : ld1(scr_r, lo, C_SLOT(16 * U + r));
+                    float cn, hn;
+                    nn_lstm_cell(s0, s1, s2, s3, s4, cold, &cn, &hn);
+                    st1(scr_r, lo, C_SLOT(16 * U + r), cn);
+                    st1(scr_r, lo, H_SLOT(16 * U + r), hn);
+                }
             }
 #pragma unroll
             for (int i = 0; i < 64; ++i) hB[i] = ld1(scr_r, lo, H_SLOT(i));
         }
+#else
+        if (t == 0) {
+#pragma unroll
+            for (int i = 0; i < 64; ++i) hB[i] = xB[i];
+        }
+#endif
         if (t == 0) continue;            // t=0 logits are discarded (nets.py:205-206)
 
         // ========== logits + log_softmax + greedy argmax (nets.py:202,208-209) ==============
-        const int nvt = (p.V1 + 31) >> 5;
+        // 64 vocab rows per LDS stage (two independent 32-row MFMA chains per wave). The two
+        // waves sharing a SIMD (w and w+4: opposite signs) run the MFMA chains and the VALU
+        // epilogue of the previous stage in opposite orders, so VALU of one wave overlaps the
+        // MFMAs of the other. Rows >= V1 read as zero through the bounded buffer resources.
+        const int nvt = (p.V1 + 31) >> 5;            // 32-row tiles (exact fallback pass)
         auto desc = [&](int n) {
             TileDesc d;
             d.w_off = (uint32_t)p.off_log_w; d.ld = 128; d.row0 = 32 * n; d.nvalid = min(32, p.V1 - 32 * n); d.k0 = 0;
             d.b_off = (uint32_t)p.off_log_b; d.pad_bias = NEG_INF;
             return d;
         };
+        const int nst = (p.V1 + 63) >> 6;
         RowState st;
         row_state_init(st);
-        stage_load(theta_r, noise_r, desc(0), tid, sr);
-        stage_store(lds, desc(0), sigma, tid, sr);
+        Stage64Regs s64;
+        stage64_load(lw_r, lz_r, lbw_r, lbz_r, 0, tid, s64);
+        stage64_store(lds, 0, p.V1, sigma, tid, s64);
         __syncthreads();
-        for (int n = 0; n < nvt; ++n) {
-            if (n + 1 < nvt) stage_load(theta_r, noise_r, desc(n + 1), tid, sr);
-            const float* buf = lds + (n & 1) * STAGE_FLOATS;
-            const f32x16 acc = mfma_tile(bias_init(buf + 2 * SIGN_FLOATS + 32 * sgn, hh), buf + sgn * SIGN_FLOATS, hB, lane);
-            if (n + 1 < nvt) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), sigma, tid, sr);
-            logit_epilogue(st, acc, 32 * n + 4 * hh);
+        f32x16 prev0, prev1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { prev0[r] = NEG_INF; prev1[r] = NEG_INF; }
+        for (int s = 0; s < nst; ++s) {
+#if !(DECODE_ABLATE & 2)
+            stage64_load(lw_r, lz_r, lbw_r, lbz_r, min(s + 1, nst - 1), tid, s64);
+#endif
+            const float* buf = lds + (s & 1) * STAGE64_FLOATS;
+            const float* wsg = buf + sgn * (64 * LDS_ROW);
+            const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * sgn;
+            f32x16 acc0, acc1;
+            if (sgn == 0) {
+                mfma_stage64(wsg, bsg, hB, lane, acc0, acc1);
+#if !(DECODE_ABLATE & 1)
+                epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * hh);
+#endif
+            } else {
+#if !(DECODE_ABLATE & 1)
+                epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * hh);
+#endif
+                mfma_stage64(wsg, bsg, hB, lane, acc0, acc1);
+            }
+#if !(DECODE_ABLATE & 2)
+            stage64_store(lds + ((s + 1) & 1) * STAGE64_FLOATS, min(s + 1, nst - 1), p.V1, sigma, tid, s64);
+#endif
+#if !(DECODE_ABLATE & 8)
             __syncthreads();
+#endif
+            prev0 = acc0;
+            prev1 = acc1;
         }
+        epilogue64(st, prev0, prev1, 64 * (nst - 1) + 4 * hh);
         // merge the two lane halves that share this batch row
         const float m_o = __shfl_xor(st.m, 32);
         const float s_o = __shfl_xor(st.s, 32);
@@ -411,6 +673,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
             tok = min(best, __shfl_xor(best, 32));
             if (tid == 0) atomicAdd(p.stats + 0, 1);
         }
+        // no candidate only when every logit is NaN (torch.max would return a NaN's index):
+        // end the caption instead of emitting an out-of-vocabulary id
+        if (tok >= p.V1) tok = 0;
         // finished mask (nets.py:236-243)
         unfinished = unfinished && (tok > 0);
         it = unfinished ? tok : 0;
@@ -424,7 +689,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
 }
 
 extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream) {
-    const size_t lds_bytes = (size_t)(2 * STAGE_FLOATS) * sizeof(float);
+    const size_t lds_bytes = (size_t)(2 * STAGE64_FLOATS) * sizeof(float);   // >= 2 * STAGE_FLOATS
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void*)nicnes_decode_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);

@@ -28,18 +28,19 @@ class NicnesError(RuntimeError):
     pass
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    """Load the in-tree engine library (built by `make -C nes-img-captioning_amd`)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise NicnesError('libnicnes.so not built: run `make -C nes-img-captioning_amd` '
-                          '(or __graft_entry__.build()); there is no CPU fallback')
-    L = ctypes.CDLL(LIB_PATH)
+def lib(path=None):
+    """Load the in-tree engine library (built by `make -C nes-img-captioning_amd`). `path` selects
+    another build of the same ABI (timing-only variants, scripts/ablate.py)."""
+    path = path or LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise NicnesError('%s not built: run `make -C nes-img-captioning_amd` '
+                          '(or __graft_entry__.build()); there is no CPU fallback' % os.path.basename(path))
+    L = ctypes.CDLL(path)
     c = ctypes
     vp, i32, i64, u64, f32, f64 = c.c_void_p, c.c_int32, c.c_int64, c.c_uint64, c.c_float, c.c_double
     sig = {
@@ -68,7 +69,7 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = L
+    _libs[path] = L
     return L
 
 

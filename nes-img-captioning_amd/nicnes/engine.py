@@ -42,10 +42,10 @@ def _ptr(t):
 class Engine:
     """One handle = one GPU. ``device`` is the local cuda index."""
 
-    def __init__(self, vocab_size=9487, input_encoding_size=128, rnn_size=128, fc_feat_size=2048,
+    def __init__(self, vocab_size=9487, input_encoding_size=128, rnn_size=128, fc_feat_size=2048,  # noqa: E501
                  seq_length=SEQ_LENGTH, max_batch=128, max_refs=None, max_members=512, noise_len=1 << 27,
-                 noise_seed=0, device=0):
-        self.L = _lib.lib()
+                 noise_seed=0, device=0, lib_path=None):
+        self.L = _lib.lib(lib_path)
         self.device = torch.device('cuda', device)
         self.cfg = NicnesConfig(vocab_size, input_encoding_size, rnn_size, fc_feat_size, seq_length, max_batch,
                                 max_refs or 8 * max_batch, max_members, noise_len, noise_seed)
