@@ -20,3 +20,5 @@ struct DecodeParams {
 
 extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream);
 extern "C" size_t nicnes_decode_scratch_floats(int member_count, int nslabs);
+extern "C" hipError_t nicnes_launch_decode_w1(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream);
+extern "C" size_t nicnes_decode_w1_scratch_floats(int member_count, int nslabs);

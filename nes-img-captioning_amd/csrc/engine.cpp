@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -60,6 +61,8 @@ struct nicnes_handle {
     double* norms = nullptr;
 
     bool timing = false;
+    int decode_variant = 2;   // 2: two waves per SIMD (decode_kernel.hip, default); 1: one wave per
+                              // SIMD, both signs per wave (decode_w1.hip, NICNES_DECODE=1)
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
 };
 
@@ -167,7 +170,15 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
     if (!rc) rc = dalloc(h, &h->ref_norm, MR * 4);
     if (!rc) rc = dalloc(h, &h->nidx, MM);
     if (!rc) rc = dalloc(h, &h->seq, MM * 2 * MB * T);
-    if (!rc) rc = dalloc(h, &h->dscratch, nicnes_decode_scratch_floats((int)MM, nslabs_of((int)MB)));
+    {
+        const char* v = getenv("NICNES_DECODE");
+        if (v && v[0] == '1') h->decode_variant = 1;
+    }
+    if (!rc) {
+        const size_t a = nicnes_decode_scratch_floats((int)MM, nslabs_of((int)MB));
+        const size_t b = nicnes_decode_w1_scratch_floats((int)MM, nslabs_of((int)MB));
+        rc = dalloc(h, &h->dscratch, a > b ? a : b);
+    }
     if (!rc) rc = dalloc(h, &h->stats, 4);
     if (!rc) rc = dalloc(h, &h->partials, 2 * (size_t)nicnes_adam_blocks(h->D));
     if (!rc) rc = dalloc(h, &h->norms, 2);
@@ -343,7 +354,8 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
     // rows a member never writes (all finished early) must read as 0 (nets.py:188 zeros)
     HIPC(h, hipMemsetAsync(p.seq, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(int32_t), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
-    HIPC(h, nicnes_launch_decode(&p, count, nslabs_of(h->B), s));
+    if (h->decode_variant == 2) HIPC(h, nicnes_launch_decode(&p, count, nslabs_of(h->B), s));
+    else HIPC(h, nicnes_launch_decode_w1(&p, count, nslabs_of(h->B), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     CiderTables tb = tables_of(h);
     HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, fitness_out, s));
