@@ -108,6 +108,16 @@ int nicnes_grad_partial(nicnes_handle* h, uint64_t iteration, int32_t member_beg
 int nicnes_adam_step(nicnes_handle* h, const float* gsum, int32_t P, double l2coeff, double stepsize, double beta1,
                      double beta2, double epsilon, double* ratio_out_host, void* stream);
 
+/* SGD with momentum in the same fused form (src/algorithm/nic_nes/optimizers.py:38-47). */
+int nicnes_sgd_step(nicnes_handle* h, const float* gsum, int32_t P, double l2coeff, double stepsize, double momentum,
+                    double* ratio_out_host, void* stream);
+
+/* Optimizer.update(globalg) (optimizers.py:15-22) with a caller-provided globalg [D] widened to
+ * fp64; globalg_fp32 = 1 when the caller's array was fp32 (numpy then keeps (1 - b) * globalg in
+ * fp32). kind 0 = Adam (beta1, beta2, epsilon), 1 = SGD (beta1 = momentum). Synchronising (ratio). */
+int nicnes_optimizer_update(nicnes_handle* h, int kind, const double* globalg, int globalg_fp32, double stepsize,
+                            double beta1, double beta2, double epsilon, double* ratio_out_host, void* stream);
+
 /* diagnostics: [0] = exact-pass fallbacks of the greedy tie rule since creation (synchronising) */
 int nicnes_stats(nicnes_handle* h, int64_t* out4_host);
 

@@ -384,9 +384,10 @@ int nicnes_grad_partial(nicnes_handle* h, uint64_t iteration, int32_t member_beg
     return NICNES_OK;
 }
 
-int nicnes_adam_step(nicnes_handle* h, const float* gsum, int32_t P, double l2coeff, double stepsize, double beta1,
-                     double beta2, double epsilon, double* ratio_out_host, void* stream) {
-    if (!h || !gsum || P < 1) return NICNES_ERR_INVALID;
+// one optimizer update (kind 0 Adam, 1 SGD), from the fused NES form (gsum, P, l2coeff) or from a
+// given globalg (Optimizer.update(globalg), optimizers.py:15-22)
+static int opt_step(nicnes_handle* h, int kind, const float* gsum, int32_t P, double l2coeff, const double* globalg,
+                    int globalg_fp32, double stepsize, double b1, double b2, double epsilon, double* ratio_out_host, void* stream) {
     if (!h->theta_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_theta first");
     hipStream_t s = (hipStream_t)stream;
     HIPC(h, hipSetDevice(h->device));
@@ -397,20 +398,25 @@ int nicnes_adam_step(nicnes_handle* h, const float* gsum, int32_t P, double l2co
     p.m = h->m;
     p.v = h->v;
     p.gsum = gsum;
+    p.globalg = globalg;
     p.partials = h->partials;
     p.dim = h->D;
-    p.two_f = (float)(2 * P);
+    p.two_f = (float)(2 * (P > 0 ? P : 1));
     p.theta_is_fp32 = h->theta_is_fp32;
     p.l2coeff = l2coeff;
     p.l2coeff32 = (float)l2coeff;
-    // a = stepsize * sqrt(1 - b2^t) / (1 - b1^t)   (optimizers.py:79, Python float arithmetic)
-    p.a = stepsize * std::sqrt(1.0 - std::pow(beta2, (double)h->t)) / (1.0 - std::pow(beta1, (double)h->t));
-    p.beta1 = beta1;
-    p.beta2 = beta2;
-    p.one_minus_beta1 = 1.0 - beta1;
-    p.one_minus_beta2 = 1.0 - beta2;
-    p.one_minus_beta1_32 = (float)(1.0 - beta1);
-    p.one_minus_beta2_32 = (float)(1.0 - beta2);
+    p.kind = kind;
+    // fused form: g' is fp32 exactly while theta is (nic_nes_master.py:126-133)
+    p.g_is_fp32 = globalg ? (globalg_fp32 != 0) : h->theta_is_fp32;
+    // Adam: a = stepsize * sqrt(1 - b2^t) / (1 - b1^t)   (optimizers.py:79, Python float arithmetic)
+    p.a = kind == 0 ? stepsize * std::sqrt(1.0 - std::pow(b2, (double)h->t)) / (1.0 - std::pow(b1, (double)h->t)) : 0.0;
+    p.neg_stepsize = -stepsize;
+    p.beta1 = b1;                      // SGD: momentum
+    p.beta2 = b2;
+    p.one_minus_beta1 = 1.0 - b1;
+    p.one_minus_beta2 = 1.0 - b2;
+    p.one_minus_beta1_32 = (float)(1.0 - b1);
+    p.one_minus_beta2_32 = (float)(1.0 - b2);
     p.epsilon = epsilon;
     HIPC(h, nicnes_launch_adam(&p, h->norms, s));
     h->theta_is_fp32 = 0;
@@ -421,6 +427,24 @@ int nicnes_adam_step(nicnes_handle* h, const float* gsum, int32_t P, double l2co
         *ratio_out_host = std::sqrt(n2[0]) / std::sqrt(n2[1]);
     }
     return NICNES_OK;
+}
+
+int nicnes_adam_step(nicnes_handle* h, const float* gsum, int32_t P, double l2coeff, double stepsize, double beta1,
+                     double beta2, double epsilon, double* ratio_out_host, void* stream) {
+    if (!h || !gsum || P < 1) return NICNES_ERR_INVALID;
+    return opt_step(h, 0, gsum, P, l2coeff, nullptr, 0, stepsize, beta1, beta2, epsilon, ratio_out_host, stream);
+}
+
+int nicnes_sgd_step(nicnes_handle* h, const float* gsum, int32_t P, double l2coeff, double stepsize, double momentum,
+                    double* ratio_out_host, void* stream) {
+    if (!h || !gsum || P < 1) return NICNES_ERR_INVALID;
+    return opt_step(h, 1, gsum, P, l2coeff, nullptr, 0, stepsize, momentum, 0.0, 0.0, ratio_out_host, stream);
+}
+
+int nicnes_optimizer_update(nicnes_handle* h, int kind, const double* globalg, int globalg_fp32, double stepsize,
+                            double beta1, double beta2, double epsilon, double* ratio_out_host, void* stream) {
+    if (!h || !globalg || (kind != 0 && kind != 1)) return NICNES_ERR_INVALID;
+    return opt_step(h, kind, nullptr, 0, 0.0, globalg, globalg_fp32, stepsize, beta1, beta2, epsilon, ratio_out_host, stream);
 }
 
 int nicnes_stats(nicnes_handle* h, int64_t* out4_host) {

@@ -18,6 +18,10 @@ struct AdamParams {
     double a;               // stepsize * sqrt(1 - b2^t) / (1 - b1^t), computed on the host
     double beta1, beta2, one_minus_beta1, one_minus_beta2, epsilon;
     float one_minus_beta1_32, one_minus_beta2_32;
+    int32_t kind;           // 0 Adam, 1 SGD with momentum (beta1 = momentum)
+    double neg_stepsize;    // SGD: -stepsize
+    const double* globalg;  // non-null: Optimizer.update(globalg) form (gsum / l2coeff unused)
+    int32_t g_is_fp32;      // globalg was an fp32 array: (1 - b) * g' products stay fp32 (NEP 50)
 };
 
 extern "C" hipError_t nicnes_launch_noise_index(uint64_t seed, uint64_t iteration, uint64_t member0, int count,

@@ -81,30 +81,45 @@ __global__ __launch_bounds__(256) void nicnes_adam_kernel(AdamParams p) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double s2 = 0.0, t2 = 0.0;
     if (j < p.dim) {
-        const float g = p.gsum[j] / p.two_f;                 // gradient_est /= ranked_fitnesses.size (fp32)
         const double th = p.theta64[j];
-        double m, v;
-        if (p.theta_is_fp32) {
-            // Before the first update theta (and so reg and g') are fp32 arrays, and numpy keeps
-            // python_float * fp32_array in fp32: (1 - b1) * g' and (1 - b2) * (g' * g') are fp32
-            // products added to the fp64 moments (optimizers.py:81-82 with NEP-50 promotion).
-            const float th32 = (float)th;
-            const float reg = p.l2coeff32 * th32;
-            const float gp = -g + reg;
-            const float t1 = p.one_minus_beta1_32 * gp;
-            const float t2 = p.one_minus_beta2_32 * (gp * gp);
-            m = p.beta1 * p.m[j] + (double)t1;
-            v = p.beta2 * p.v[j] + (double)t2;
+        // globalg g' = -g + l2coeff * theta (nic_nes_master.py:311-318), or given directly
+        // (Optimizer.update(globalg)). Before the first update theta, and so g', are fp32 arrays.
+        float gp32 = 0.f;
+        double gp64;
+        if (p.globalg) {
+            gp64 = p.globalg[j];
+            gp32 = (float)gp64;
         } else {
-            const double reg = p.l2coeff * th;
-            const double gp = (double)(-g) + reg;
-            m = p.beta1 * p.m[j] + p.one_minus_beta1 * gp;
-            v = p.beta2 * p.v[j] + p.one_minus_beta2 * (gp * gp);
+            const float g = p.gsum[j] / p.two_f;             // gradient_est /= ranked_fitnesses.size (fp32)
+            if (p.theta_is_fp32) {
+                gp32 = -g + p.l2coeff32 * (float)th;
+                gp64 = gp32;
+            } else {
+                gp64 = (double)(-g) + p.l2coeff * th;
+            }
         }
-        const double step = (-p.a * m) / (sqrt(v) + p.epsilon);
+        // numpy keeps python_float * fp32_array in fp32 (NEP 50): at the first update the
+        // (1 - b) * g' products are fp32, added to the fp64 state (optimizers.py:45,81-82)
+        double step;
+        if (p.kind == 0) {                                   // Adam._compute_step, optimizers.py:78-83
+            double m, v;
+            if (p.g_is_fp32) {
+                m = p.beta1 * p.m[j] + (double)(p.one_minus_beta1_32 * gp32);
+                v = p.beta2 * p.v[j] + (double)(p.one_minus_beta2_32 * (gp32 * gp32));
+            } else {
+                m = p.beta1 * p.m[j] + p.one_minus_beta1 * gp64;
+                v = p.beta2 * p.v[j] + p.one_minus_beta2 * (gp64 * gp64);
+            }
+            step = (-p.a * m) / (sqrt(v) + p.epsilon);
+            p.m[j] = m;
+            p.v[j] = v;
+        } else {                                             // SGD._compute_step, optimizers.py:44-47
+            const double v = p.g_is_fp32 ? p.beta1 * p.v[j] + (double)(p.one_minus_beta1_32 * gp32)
+                                             : p.beta1 * p.v[j] + p.one_minus_beta1 * gp64;
+            step = p.neg_stepsize * v;
+            p.v[j] = v;
+        }
         const double nt = th + step;
-        p.m[j] = m;
-        p.v[j] = v;
         p.theta64[j] = nt;
         p.theta32[j] = (float)nt;
         s2 = step * step;

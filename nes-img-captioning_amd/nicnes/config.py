@@ -1,0 +1,103 @@
+"""The reference's experiment-JSON surface, read for the engine.
+
+Field names and defaults mirror
+  Config            /root/reference/src/algorithm/tools/utils.py:14-20
+  PolicyOptions     /root/reference/src/algorithm/policies.py:31-34
+  ModelOptions      /root/reference/src/algorithm/policies.py:36-41
+  optimizer_options /root/reference/src/algorithm/nic_nes/experiment.py:20-21
+A leading underscore disables a key ("_from_infos"), as in the reference JSON files. The engine
+implements the mscoco_nes.json hot path only: net 'fc_caption', fitness 'greedy', no vbn /
+layer_n / safe mutations; anything else raises NotSupported (nicnes_create returns
+NICNES_ERR_UNSUPPORTED for unsupported model sizes).
+"""
+import json
+from collections import namedtuple
+
+config_fields = [
+    'l2coeff', 'noise_stdev', 'stdev_divisor', 'eval_prob', 'snapshot_freq', 'log_dir',
+    'batch_size', 'patience', 'val_batch_size', 'num_val_batches',
+    'num_val_items', 'cuda', 'max_nb_iterations', 'ref_batch_size', 'bs_multiplier', 'stepsize_divisor',
+    'single_batch', 'schedule_limit', 'schedule_start'
+]
+Config = namedtuple('Config', field_names=config_fields, defaults=(None,) * len(config_fields))
+
+_opt_fields = ['net', 'safe_mutations', 'model_options', 'safe_mutation_underflow', 'fitness',
+               'vbn', 'safe_mutation_batch_size', 'safe_mutation_vector']
+PolicyOptions = namedtuple('PolicyOptions', field_names=_opt_fields,
+                           defaults=[None, '', {}, 0.01, None, False, 32, None])
+
+_model_opt_fields = ['vocab_size', 'input_encoding_size', 'rnn_type', 'rnn_size', 'num_layers',
+                     'drop_prob_lm', 'seq_length', 'fc_feat_size', 'vbn', 'vbn_e', 'vbn_affine', 'layer_n',
+                     'layer_n_affine', 'safe_mutation_underflow', 'safe_mutations', 'safe_mutation_vector',
+                     'safe_mutation_batch_size']
+ModelOptions = namedtuple('ModelOptions', field_names=_model_opt_fields, defaults=(0,) * len(_model_opt_fields))
+
+
+class NotSupported(ValueError):
+    pass
+
+
+def load_experiment(path_or_dict):
+    """JSON file or dict -> dict with disabled ('_'-prefixed) top-level keys dropped."""
+    exp = path_or_dict
+    if not isinstance(exp, dict):
+        with open(path_or_dict) as f:
+            exp = json.load(f)
+    return {k: v for k, v in exp.items() if not k.startswith('_')}
+
+
+class ExperimentSpec:
+    """What the engine needs from an experiment JSON (mscoco_nes.json and variants)."""
+
+    def __init__(self, exp, vocab_size=9487, seq_length=16):
+        exp = load_experiment(exp)
+        if exp.get('algorithm', 'nic_nes') != 'nic_nes':
+            raise NotSupported('algorithm %r: the engine implements nic_nes' % exp.get('algorithm'))
+        if exp.get('dataset', 'mscoco') != 'mscoco':
+            raise NotSupported('dataset %r: the engine implements the mscoco fc_caption path' % exp.get('dataset'))
+        self.exp = exp
+        self.config = Config(**exp['config'])
+        po = dict(exp['policy_options'])
+        self.policy_options = PolicyOptions(**po)
+        mo = dict(po.get('model_options', {}))
+        mo.setdefault('vocab_size', vocab_size)          # injected from data, captioning/experiment.py:27-30
+        mo.setdefault('seq_length', seq_length)
+        self.model_options = ModelOptions(**{k: v for k, v in mo.items() if k in _model_opt_fields})
+        self._validate()
+        opt = exp.get('optimizer_options', {'type': 'adam', 'args': {'stepsize': 1e-3}})
+        self.optimizer_type = opt['type']
+        self.optimizer_args = dict(opt.get('args', {}))
+        if self.optimizer_type not in ('adam', 'sgd'):
+            raise NotSupported('optimizer %r' % self.optimizer_type)
+        self.nb_offspring = int(exp.get('nb_offspring', 1))
+
+    def _validate(self):
+        po, mo = self.policy_options, self.model_options
+        if po.net != 'fc_caption':
+            raise NotSupported('net %r: the engine implements fc_caption' % po.net)
+        if (po.fitness or 'greedy') != 'greedy':
+            raise NotSupported("fitness %r: the engine implements 'greedy' (100 * mean CIDEr-D)" % po.fitness)
+        if po.vbn or mo.vbn_e or mo.layer_n:
+            raise NotSupported('virtual batch norm / layer norm are not implemented by the engine')
+        if (po.safe_mutations or '') or (mo.safe_mutations or ''):
+            raise NotSupported('safe mutations are not implemented by the engine')
+
+    # ------------------------------------------------------------------------------------
+    @property
+    def sigma(self):
+        return float(self.config.noise_stdev)
+
+    @property
+    def batch_size(self):
+        return int(self.config.batch_size)
+
+    @property
+    def l2coeff(self):
+        return float(self.config.l2coeff or 0.0)
+
+    def engine_kwargs(self, max_members, noise_len=1 << 27, noise_seed=0, max_batch=None):
+        mo = self.model_options
+        return dict(vocab_size=int(mo.vocab_size), input_encoding_size=int(mo.input_encoding_size or 128),
+                    rnn_size=int(mo.rnn_size or 128), fc_feat_size=int(mo.fc_feat_size or 2048),
+                    seq_length=int(mo.seq_length or 16), max_batch=int(max_batch or self.batch_size),
+                    max_members=int(max_members), noise_len=int(noise_len), noise_seed=int(noise_seed))

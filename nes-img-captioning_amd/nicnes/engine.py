@@ -190,6 +190,25 @@ class Engine:
                                           ctypes.byref(ratio), self._stream()), self.h, 'adam_step')
         return ratio.value
 
+    def sgd_step(self, gsum, P, l2coeff, stepsize, momentum=0.9):
+        ratio = ctypes.c_double()
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_sgd_step(self.h, _ptr(gsum), P, l2coeff, stepsize, momentum, ctypes.byref(ratio),
+                                         self._stream()), self.h, 'sgd_step')
+        return ratio.value
+
+    def optimizer_update(self, globalg, kind='adam', stepsize=1e-3, beta1=0.9, beta2=0.999, epsilon=1e-08):
+        """Optimizer.update(globalg) form: globalg [D] fp32 or fp64 -> update ratio."""
+        is32 = (globalg.dtype == torch.float32) if isinstance(globalg, torch.Tensor) else \
+            (np.asarray(globalg).dtype == np.float32)
+        g = self._dev(globalg, torch.float64)
+        ratio = ctypes.c_double()
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_optimizer_update(self.h, {'adam': 0, 'sgd': 1}[kind], _ptr(g), int(is32), stepsize,
+                                                 beta1, beta2, epsilon, ctypes.byref(ratio), self._stream()), self.h,
+                  'optimizer_update')
+        return ratio.value
+
     def set_timing(self, on=True):
         check(self.L.nicnes_set_timing(self.h, int(bool(on))), self.h, 'set_timing')
 

@@ -1,0 +1,285 @@
+"""Master/worker transport for the engine, mirroring /root/reference/src/dist.py.
+
+Same keys (dist.py:17-22) and the same client methods (MasterClient.declare_experiment /
+declare_task / pop_result / flush_results, WorkerClient.get_experiment / get_current_task /
+push_result, dist.py:68-201), with two deliberate differences:
+
+* the wire codec is msgpack with an ndarray extension (dtype string, shape, raw bytes) instead of
+  pickle (dist.py:25-30): a message can carry only plain data, decoding never executes anything;
+* results are ~100 bytes (fitness pair + noise index) instead of the 11.46 MB noise vector.
+
+`LocalStore` is an in-process, thread-safe subset of the redis commands these clients use, so a
+master and its workers can run in one process (tests, single-node) without a redis server. A real
+redis server is used when the `redis` package is importable and a redis config dict is given.
+"""
+import threading
+import time
+from collections import deque
+
+import msgpack
+import numpy as np
+
+from .nes import NESResult, NESTask
+
+EXP_KEY = 'nic:exp'
+TASK_ID_KEY = 'nic:task_id'
+TASK_DATA_KEY = 'nic:task_data'
+TASK_CHANNEL = 'nic:task_channel'
+RESULTS_KEY = 'nic:results'
+ARCHIVE_KEY = 'nic:archive'
+MEMBER_KEY = 'nic:member_counter'       # new: per-task member-id allocator (members are noise indices)
+
+_EXT_NDARRAY, _EXT_TASK, _EXT_RESULT, _EXT_TUPLE = 1, 2, 3, 4
+
+
+# ---------------------------------------------------------------- codec ---------------------------
+def _default(obj):
+    if isinstance(obj, NESTask):
+        return msgpack.ExtType(_EXT_TASK, serialize(list(obj)))
+    if isinstance(obj, NESResult):
+        return msgpack.ExtType(_EXT_RESULT, serialize(list(obj)))
+    if isinstance(obj, tuple):
+        return msgpack.ExtType(_EXT_TUPLE, serialize(list(obj)))
+    if isinstance(obj, np.ndarray):
+        if obj.dtype.hasobject:
+            raise TypeError('object arrays cannot be sent')
+        a = np.ascontiguousarray(obj)
+        return msgpack.ExtType(_EXT_NDARRAY, msgpack.packb([a.dtype.str, list(a.shape), a.tobytes()]))
+    if isinstance(obj, np.generic):
+        return obj.item()
+    if hasattr(obj, 'detach') and hasattr(obj, 'numpy'):          # torch tensor -> ndarray
+        return _default(obj.detach().cpu().numpy())
+    raise TypeError('cannot serialize %r' % type(obj))
+
+
+def _ext_hook(code, data):
+    if code == _EXT_NDARRAY:
+        dt, shape, raw = msgpack.unpackb(data)
+        dt = np.dtype(dt)
+        if dt.hasobject:
+            raise ValueError('object dtype on the wire')
+        return np.frombuffer(raw, dtype=dt).reshape(shape).copy()
+    if code == _EXT_TASK:
+        return NESTask(*deserialize(data))
+    if code == _EXT_RESULT:
+        return NESResult(*deserialize(data))
+    if code == _EXT_TUPLE:
+        return tuple(deserialize(data))
+    raise ValueError('unknown extension type %d' % code)
+
+
+def serialize(x):
+    return msgpack.packb(x, default=_default, use_bin_type=True, strict_types=True)
+
+
+def deserialize(b):
+    return msgpack.unpackb(b, ext_hook=_ext_hook, raw=False, strict_map_key=False)
+
+
+# ---------------------------------------------------------------- in-process store ----------------
+class _Pipeline:
+    def __init__(self, store):
+        self.s, self.ops = store, []
+
+    def __getattr__(self, name):
+        fn = getattr(self.s, name)
+
+        def queue(*a, **k):
+            self.ops.append((fn, a, k))
+            return self
+        return queue
+
+    def watch(self, *keys):
+        return None
+
+    def multi(self):
+        return None
+
+    def execute(self):
+        with self.s._cv:
+            out = [fn(*a, **k) for fn, a, k in self.ops]
+        self.ops = []
+        return out
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.ops = []
+        return False
+
+
+class LocalStore:
+    """The redis subset dist.py uses: get/set/mget/mset/incrby/rpush/blpop/llen/ltrim/lrange/publish."""
+
+    def __init__(self):
+        self._kv, self._lists = {}, {}
+        self._cv = threading.Condition(threading.RLock())
+
+    def ping(self):
+        return True
+
+    def set(self, k, v):
+        with self._cv:
+            self._kv[k] = v if isinstance(v, bytes) else str(v).encode()
+            return True
+
+    def get(self, k):
+        with self._cv:
+            return self._kv.get(k)
+
+    def mget(self, keys):
+        with self._cv:
+            return [self._kv.get(k) for k in keys]
+
+    def mset(self, mapping):
+        with self._cv:
+            for k, v in mapping.items():
+                self.set(k, v)
+            return True
+
+    def delete(self, *keys):
+        with self._cv:
+            n = 0
+            for k in keys:
+                n += int(self._kv.pop(k, None) is not None) + int(self._lists.pop(k, None) is not None)
+            return n
+
+    def incrby(self, k, n=1):
+        with self._cv:
+            v = int(self._kv.get(k, b'0')) + int(n)
+            self._kv[k] = str(v).encode()
+            return v
+
+    def rpush(self, k, *vals):
+        with self._cv:
+            q = self._lists.setdefault(k, deque())
+            q.extend(vals)
+            self._cv.notify_all()
+            return len(q)
+
+    def blpop(self, k, timeout=0):
+        deadline = None if not timeout else time.monotonic() + timeout
+        with self._cv:
+            while not self._lists.get(k):
+                left = None if deadline is None else deadline - time.monotonic()
+                if left is not None and left <= 0:
+                    return None
+                self._cv.wait(left)
+            return (k, self._lists[k].popleft())
+
+    def llen(self, k):
+        with self._cv:
+            return len(self._lists.get(k, ()))
+
+    def ltrim(self, k, start, end):
+        with self._cv:
+            q = list(self._lists.get(k, ()))
+            n = len(q)
+            s = start if start >= 0 else max(n + start, 0)
+            e = end if end >= 0 else n + end
+            self._lists[k] = deque(q[s:e + 1])
+            return True
+
+    def lrange(self, k, start, end):
+        with self._cv:
+            q = list(self._lists.get(k, ()))
+            e = end if end >= 0 else len(q) + end
+            return q[start:e + 1]
+
+    def publish(self, channel, msg):
+        return 0
+
+    def pipeline(self):
+        return _Pipeline(self)
+
+
+def connect(cfg):
+    """LocalStore / redis-like object -> itself; dict -> redis.StrictRedis(**cfg) (needs redis-py)."""
+    if cfg is None:
+        return LocalStore()
+    if hasattr(cfg, 'rpush'):
+        return cfg
+    try:
+        import redis
+    except ImportError as e:   # pragma: no cover - redis-py is absent from this image
+        raise RuntimeError('a redis config was given but the redis package is not installed') from e
+    r = redis.StrictRedis(**cfg)
+    r.ping()
+    return r
+
+
+def _retry_get(store, key, tries=300, delay=0.05):
+    for _ in range(tries):
+        if isinstance(key, (list, tuple)):
+            vals = store.mget(key)
+            if all(v is not None for v in vals):
+                return vals
+        else:
+            v = store.get(key)
+            if v is not None:
+                return v
+        time.sleep(delay)
+    raise RuntimeError('{} not set'.format(key))
+
+
+# ---------------------------------------------------------------- clients -------------------------
+class MasterClient:
+    def __init__(self, master_redis_cfg=None):
+        self.task_counter = 0
+        self.master_redis = connect(master_redis_cfg)
+
+    def declare_experiment(self, exp):
+        self.master_redis.set(EXP_KEY, serialize(exp))
+
+    def declare_task(self, task_data):
+        task_id = self.task_counter
+        self.task_counter += 1
+        data = serialize(task_data)
+        (self.master_redis.pipeline()
+         .mset({TASK_ID_KEY: task_id, TASK_DATA_KEY: data, MEMBER_KEY + ':%d' % task_id: 0})
+         .publish(TASK_CHANNEL, serialize((task_id, data)))
+         .execute())
+        return task_id
+
+    def pop_result(self, timeout=0):
+        item = self.master_redis.blpop(RESULTS_KEY, timeout=timeout)
+        if item is None:
+            return None, None
+        task_id, result = deserialize(item[1])
+        return task_id, result
+
+    def flush_results(self):
+        return max(self.master_redis.pipeline().llen(RESULTS_KEY).ltrim(RESULTS_KEY, -1, -1).execute()[0] - 1, 0)
+
+
+class WorkerClient:
+    """Argument order as in dist.py:162 (relay, master); with one store both are the same."""
+
+    def __init__(self, relay_redis_cfg=None, master_redis_cfg=None):
+        self.local_redis = connect(relay_redis_cfg)
+        self.master_redis = self.local_redis if master_redis_cfg is None else connect(master_redis_cfg)
+        self.cached_task_id, self.cached_task_data = None, None
+
+    def get_experiment(self):
+        return deserialize(_retry_get(self.local_redis, EXP_KEY))
+
+    def get_current_task(self):
+        task_id = int(_retry_get(self.local_redis, TASK_ID_KEY))
+        if task_id != self.cached_task_id:
+            tid, data = self.local_redis.mget([TASK_ID_KEY, TASK_DATA_KEY])
+            if int(tid) == task_id:
+                self.cached_task_id, self.cached_task_data = task_id, deserialize(data)
+        return self.cached_task_id, self.cached_task_data
+
+    def claim_members(self, task_id, count):
+        """Atomically reserve member ids [begin, begin+count) of this task (new; members = noise indices)."""
+        end = self.master_redis.incrby(MEMBER_KEY + ':%d' % task_id, count)
+        return end - count
+
+    def push_result(self, task_id, result):
+        self.local_redis.rpush(RESULTS_KEY, serialize((task_id, result)))
+
+    def push_results(self, task_id, results):
+        if results:
+            self.local_redis.rpush(RESULTS_KEY, *[serialize((task_id, r)) for r in results])

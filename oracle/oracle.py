@@ -231,6 +231,25 @@ class AdamOracle:
         return ratio, self.theta
 
 
+class SGDOracle:
+    """optimizers.py:38-47 (SGD with momentum), fp64 state."""
+
+    def __init__(self, theta, stepsize, momentum=0.9):
+        self.theta = theta
+        self.dim = len(theta)
+        self.t = 0
+        self.stepsize, self.momentum = stepsize, momentum
+        self.v = np.zeros(self.dim, dtype=np.float64)
+
+    def update(self, globalg):
+        self.t += 1
+        self.v = self.momentum * self.v + (1. - self.momentum) * globalg
+        step = -self.stepsize * self.v
+        ratio = np.linalg.norm(step) / np.linalg.norm(self.theta)
+        self.theta = self.theta + step
+        return ratio, self.theta
+
+
 def master_update(adam, g, l2coeff):
     """nic_nes_master.py:126-133: reg = l2coeff * theta (theta fp32 before the first update,
     fp64 after: fact 8 of SURVEY.md), globalg = -g + reg."""

@@ -15,6 +15,10 @@ Fixtures (all .npz, loadable with allow_pickle=False):
   adam.npz                        Adam.update (src/algorithm/nic_nes/optimizers.py:15-22,78-83) driven
                                   like NESMaster.run_master (nic_nes_master.py:126-133), 3 steps
   ranks.npz                       compute_centered_ranks docstring known answer (nic_nes_master.py:187-189)
+  sgd.npz                         SGD.update (optimizers.py:38-47) driven like run_master, 3 steps
+  adam_globalg64.npz              Adam.update(globalg) called directly with an fp64 globalg from the
+                                  first step (the fp64 (1 - b) * g' branch while theta is still fp32)
+Pass fixture names to regenerate a subset: python scripts/make_golden.py sgd adam_globalg64
 """
 import json
 import os
@@ -148,6 +152,46 @@ def adam_fixture():
     print('adam ok, ratio', ratios)
 
 
+def sgd_fixture():
+    np.float = float
+    from algorithm.nic_nes.optimizers import SGD    # reference module
+    rng = np.random.Generator(np.random.PCG64(98))
+    D = 1000
+    theta32 = rng.standard_normal(D).astype(np.float32)
+    grads = rng.standard_normal((3, D)).astype(np.float32) * np.float32(0.05)
+    l2coeff, stepsize, momentum = 1e-3, 1e-2, 0.9
+    opt = SGD(theta32.copy(), stepsize, momentum)
+    theta = theta32.copy()
+    thetas, ratios, vs = [], [], []
+    for k in range(3):
+        reg = l2coeff * theta
+        ratio, theta = opt.update(-grads[k] + reg)
+        thetas.append(np.asarray(theta, np.float64))
+        ratios.append(ratio)
+        vs.append(opt.v.copy())
+    np.savez_compressed(os.path.join(OUT, 'sgd.npz'), theta0=theta32, grads=grads, l2coeff=np.float64(l2coeff),
+                        stepsize=np.float64(stepsize), momentum=np.float64(momentum), thetas=np.stack(thetas),
+                        ratios=np.array(ratios), vs=np.stack(vs))
+    print('sgd ok, ratio', ratios)
+
+
+def adam_globalg64_fixture():
+    np.float = float
+    from algorithm.nic_nes.optimizers import Adam   # reference module
+    rng = np.random.Generator(np.random.PCG64(97))
+    D = 1000
+    theta32 = rng.standard_normal(D).astype(np.float32)
+    globalgs = rng.standard_normal((2, D)) * 0.05          # fp64
+    opt = Adam(theta32.copy(), 1e-2)
+    thetas = []
+    for k in range(2):
+        _, theta = opt.update(globalgs[k])
+        thetas.append(np.asarray(theta, np.float64))
+    np.savez_compressed(os.path.join(OUT, 'adam_globalg64.npz'), theta0=theta32, globalgs=globalgs,
+                        stepsize=np.float64(1e-2), thetas=np.stack(thetas), m=opt.m.copy(), v=opt.v.copy())
+    print('adam_globalg64 ok')
+
+
 def ranks_fixture():
     # docstring known answer, /root/reference/src/algorithm/nic_nes/nic_nes_master.py:187-189
     x = np.array([[101, 200], [2, 100]], np.float64)
@@ -155,7 +199,7 @@ def ranks_fixture():
     np.savez_compressed(os.path.join(OUT, 'ranks.npz'), x=x, y=y)
 
 
-if __name__ == '__main__':
+def all_fixtures():
     tiny = O.Dims(vocab_size=63, E=32, R=32, F=64)
     full = O.Dims()
     decode_fixture('decode_tiny_xavier', tiny, 1, 1.0, 0.0, 1234, 8, True)
@@ -165,6 +209,16 @@ if __name__ == '__main__':
     perturb_fixture()
     adam_fixture()
     ranks_fixture()
+    sgd_fixture()
+    adam_globalg64_fixture()
+
+
+if __name__ == '__main__':
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()[name + '_fixture']()
+    else:
+        all_fixtures()
     with open(os.path.join(OUT, 'MANIFEST.json'), 'w') as f:
         json.dump({'generator': 'scripts/make_golden.py', 'reference': 'rubencart/NES-img-captioning @ /root/reference',
                    'torch': torch.__version__, 'numpy': np.__version__, 'threads': 1}, f, indent=1)

@@ -7,15 +7,55 @@ from oracle import cider_ref as CR
 from oracle import oracle as O
 
 
+class _Cfg:
+    def __init__(self, dims):
+        self.vocab_size, self.input_encoding_size, self.rnn_size, self.fc_feat_size = dims.vocab_size, dims.E, \
+            dims.R, dims.F
+        self.seq_length = 16
+
+
 class OracleEngine:
     def __init__(self, dims, theta32, fc, gts, df, ref_len_raw, table, noise_seed=0):
         self.device = torch.device('cpu')
         self.dims, self.D = dims, dims.D
+        self.cfg = _Cfg(dims)
         self.fc, self.gts, self.table, self.seed = fc, gts, table, noise_seed
         self.scorer = CR.CiderDOracle(df, ref_len_raw)
         self.adam = None
         self.theta32 = theta32.copy()
         self.theta_src = theta32.copy()
+
+    # ---- Engine surface used by nicnes.nes / nicnes.master
+    def set_theta(self, theta, fp32_origin=None):
+        th = theta.numpy() if isinstance(theta, torch.Tensor) else np.asarray(theta)
+        self.theta_src = th.copy()
+        self.theta32 = th.astype(np.float32)
+        self.adam = None
+
+    def theta(self):
+        src = self.adam.theta if self.adam is not None else self.theta_src
+        return torch.from_numpy(np.asarray(src, np.float64).copy()), torch.from_numpy(self.theta32.copy())
+
+    def set_batch(self, fc, gts):
+        self.fc, self.gts = np.asarray(fc, np.float32), gts
+
+    def noise_indices(self, iteration, member_begin, count):
+        return torch.tensor([self._idx(iteration, member_begin + k) for k in range(count)], dtype=torch.int64)
+
+    def adam_state(self):
+        if self.adam is None:
+            z = torch.zeros(self.D, dtype=torch.float64)
+            return z, z.clone(), 0
+        m = getattr(self.adam, 'm', np.zeros(self.D))
+        return torch.from_numpy(np.asarray(m, np.float64)), torch.from_numpy(self.adam.v.copy()), self.adam.t
+
+    def sgd_step(self, gsum, P, l2coeff, stepsize, momentum=0.9):
+        if self.adam is None:
+            self.adam = O.SGDOracle(self.theta_src.copy(), stepsize, momentum)
+        g = gsum.numpy().astype(np.float32) / np.float32(2 * P)
+        ratio, theta = O.master_update(self.adam, g, l2coeff)
+        self.theta32 = np.asarray(theta).astype(np.float32)
+        return float(ratio)
 
     def _idx(self, iteration, m):
         return O.noise_index(self.seed, iteration, m, self.table.size, self.D)

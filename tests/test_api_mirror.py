@@ -1,0 +1,235 @@
+"""CPU tests of the reference-facing layer: experiment JSON surface, wire codec and in-process
+store, theta <-> state_dict, optimizer files, and the master/worker loops (dispatched over the
+transport vs the sharded local loop) on the oracle-backed CPU engine."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from nicnes import config as C
+from nicnes import master as M
+from nicnes import nes as N
+from nicnes import transport as T
+from tests.cpu_engine import OracleEngine, tiny_workload
+
+# the keys of /root/reference/experiments/mscoco_nes.json (values as in that file)
+MSCOCO_NES = {
+    'algorithm': 'nic_nes',
+    'config': {'eval_prob': 0.003, 'noise_stdev': 0.01, 'snapshot_freq': 5, 'batch_size': 64, 'val_batch_size': 256,
+               'num_val_items': 5000, 'patience': 0, 'schedule_start': 1000, 'schedule_limit': 1000,
+               'stdev_divisor': 1, 'bs_multiplier': 1, 'stepsize_divisor': 1, 'ref_batch_size': 0, 'l2coeff': 1e-7,
+               'single_batch': False},
+    'policy_options': {'net': 'fc_caption', 'fitness': 'greedy', 'vbn': False,
+                       'model_options': {'safe_mutations': '', 'safe_mutation_vector': '',
+                                         'safe_mutation_underflow': 0.1, 'vbn_e': False, 'vbn_affine': False,
+                                         'layer_n': False, 'layer_n_affine': False, 'input_encoding_size': 128,
+                                         'rnn_size': 128, 'fc_feat_size': 2048}},
+    'optimizer_options': {'type': 'adam', 'args': {'stepsize': 0.001}},
+    'dataset': 'mscoco', 'nb_offspring': 2000, 'num_elites': 1, 'from_single': './pretrained/bu_xent_09.pth',
+    '_from_infos': 'logs/x/snapshot/z_info_e1_i716-885.json',
+}
+
+
+def _exp(**over):
+    import copy
+    e = copy.deepcopy(MSCOCO_NES)
+    for k, v in over.items():
+        if isinstance(v, dict) and isinstance(e.get(k), dict):
+            e[k].update(v)
+        else:
+            e[k] = v
+    return e
+
+
+# ------------------------------------------------------------------ config -------------------------
+def test_spec_reads_mscoco_nes():
+    s = C.ExperimentSpec(MSCOCO_NES)
+    assert s.sigma == 0.01 and s.batch_size == 64 and s.l2coeff == 1e-7 and s.nb_offspring == 2000
+    assert s.optimizer_type == 'adam' and s.optimizer_args == {'stepsize': 0.001}
+    assert 'from_infos' not in s.exp and '_from_infos' not in s.exp
+    kw = s.engine_kwargs(max_members=512)
+    assert (kw['vocab_size'], kw['input_encoding_size'], kw['rnn_size'], kw['fc_feat_size'], kw['seq_length']) == \
+        (9487, 128, 128, 2048, 16)
+
+
+@pytest.mark.parametrize('over', [
+    {'policy_options': {'net': 'fc_caption', 'fitness': 'sample'}},
+    {'policy_options': {'net': 'att_caption'}},
+    {'policy_options': {'net': 'fc_caption', 'vbn': True}},
+    {'policy_options': {'net': 'fc_caption', 'model_options': {'safe_mutations': 'SM-G-SUM'}}},
+    {'optimizer_options': {'type': 'rmsprop', 'args': {}}},
+    {'algorithm': 'nic_es'},
+])
+def test_spec_rejects_unsupported(over):
+    with pytest.raises(C.NotSupported):
+        C.ExperimentSpec(_exp(**over))
+
+
+# ------------------------------------------------------------------ codec / store ------------------
+def test_codec_roundtrip_task_and_result():
+    gts = [np.arange(32, dtype=np.int64).reshape(2, 16), np.zeros((5, 16), np.int64)]
+    task = N.NESTask(current='/tmp/x.pth', batch_data={'fc_feats': np.ones((10, 8), np.float32), 'gts': gts},
+                     noise_stdev=0.01, batch_size=2, iteration=3)
+    t2 = T.deserialize(T.serialize((7, task)))
+    assert t2[0] == 7 and isinstance(t2[1], N.NESTask)
+    b = t2[1].batch_data
+    assert b['fc_feats'].dtype == np.float32 and np.array_equal(b['fc_feats'], task.batch_data['fc_feats'])
+    assert all(np.array_equal(x, y) and x.dtype == y.dtype for x, y in zip(b['gts'], gts))
+    assert t2[1].noise_stdev == 0.01 and t2[1].iteration == 3 and t2[1].ref_batch is None
+    r = N.NESResult(worker_id=5, fitness=np.array([1.5, 2.5]), noise_idx=np.int64(640), member=3)
+    r2 = T.deserialize(T.serialize(r))
+    assert isinstance(r2, N.NESResult) and r2.noise_idx == 640 and np.array_equal(r2.fitness, r.fitness)
+    assert r2.evolve_noise is None
+
+
+def test_codec_refuses_objects():
+    with pytest.raises(TypeError):
+        T.serialize(np.array([object()], dtype=object))
+    with pytest.raises(TypeError):
+        T.serialize({'f': lambda: 0})
+    import msgpack
+    with pytest.raises(ValueError):
+        T.deserialize(msgpack.packb(msgpack.ExtType(99, b'')))
+
+
+def test_local_store_semantics():
+    s = T.LocalStore()
+    assert s.blpop('q', timeout=0.01) is None
+    s.rpush('q', b'a', b'b', b'c')
+    assert s.llen('q') == 3 and s.blpop('q')[1] == b'a'
+    # MasterClient.flush_results keeps the last element and reports how many were dropped
+    mc = T.MasterClient(s)
+    s.rpush(T.RESULTS_KEY, b'1', b'2', b'3')
+    assert mc.flush_results() == 2 and s.llen(T.RESULTS_KEY) == 1
+    assert s.incrby('c', 4) == 4 and s.incrby('c', 4) == 8
+    out = s.pipeline().mset({'x': 1}).get('x').execute()
+    assert out[1] == b'1'
+
+
+def test_clients_task_cache_and_member_claims():
+    s = T.LocalStore()
+    mc, wc = T.MasterClient(s), T.WorkerClient(s)
+    mc.declare_experiment({'a': 1})
+    assert wc.get_experiment() == {'a': 1}
+    t0 = mc.declare_task(N.NESTask(noise_stdev=0.5))
+    assert wc.get_current_task()[0] == t0 == 0
+    assert wc.claim_members(t0, 8) == 0 and wc.claim_members(t0, 8) == 8
+    t1 = mc.declare_task(N.NESTask(noise_stdev=0.25))
+    tid, task = wc.get_current_task()
+    assert tid == t1 == 1 and task.noise_stdev == 0.25
+    assert wc.claim_members(t1, 4) == 0
+    wc.push_result(t1, N.NESResult(fitness=np.zeros(2), member=0))
+    tid, res = mc.pop_result(timeout=1)
+    assert tid == 1 and res.member == 0
+
+
+# ------------------------------------------------------------------ policy / optimizer files -------
+@pytest.fixture(scope='module')
+def workload():
+    return tiny_workload(B=4)
+
+
+def _engine(workload):
+    dims, theta, fc, gts, df, n, table = workload
+    return OracleEngine(dims, theta, fc, gts, df, np.log(float(n)), table)
+
+
+def test_state_dict_roundtrip_and_set_model(workload, tmp_path):
+    e = _engine(workload)
+    pol = N.EnginePolicy(e)
+    sd = pol.state_dict()
+    assert list(sd) == N.PARAM_NAMES
+    assert all(tuple(sd[k].shape) == shp for k, shp in N.param_shapes(e).items())
+    vec = N.vector_from_state_dict(sd, N.param_shapes(e))
+    assert np.array_equal(vec.numpy(), workload[1])
+    p = str(tmp_path / 'cur.pth')
+    sd64 = {k: v.double() * 2 for k, v in sd.items()}
+    torch.save(sd64, p)
+    pol.set_model(p)
+    assert np.array_equal(e.theta32, (workload[1].astype(np.float64) * 2).astype(np.float32))
+    bad = dict(sd)
+    bad.pop('core.h2h.bias')
+    with pytest.raises(KeyError):
+        pol.set_model(bad)
+    bad = dict(sd, **{'logit.bias': torch.zeros(3)})
+    with pytest.raises(ValueError):
+        pol.set_model(bad)
+
+
+def test_unique_batch():
+    fc = np.arange(40, dtype=np.float32).reshape(10, 4)
+    gts = [np.zeros((5, 16)), np.zeros((5, 16))]
+    u, g = N.unique_batch({'fc_feats': fc, 'gts': gts})
+    assert u.shape == (2, 4) and np.array_equal(u, fc[[0, 5]])
+    with pytest.raises(ValueError):
+        N.unique_batch({'fc_feats': fc[:3], 'gts': gts})
+
+
+def test_optimizer_file_reads_reference_layout(tmp_path):
+    """The reference saves m, v as numpy arrays (optimizers.py:85-95); they load under weights_only."""
+    p = str(tmp_path / 'optimizer.tar')
+    m, v = np.linspace(0, 1, 7), np.linspace(1, 2, 7)
+    torch.save({'dim': 7, 't': 3, 'stepsize': 0.5, 'beta1': 0.8, 'beta2': 0.9, 'epsilon': 1e-6, 'm': m, 'v': v}, p)
+    st = N._load_state(p)
+    assert st['t'] == 3 and np.array_equal(st['m'], m) and np.array_equal(st['v'], v)
+
+
+# ------------------------------------------------------------------ master loops ---------------------
+def _spec(P, opt='adam'):
+    return C.ExperimentSpec(_exp(nb_offspring=P, config={'noise_stdev': 0.05, 'batch_size': 4, 'l2coeff': 1e-3,
+                                                         'snapshot_freq': 1},
+                                 optimizer_options={'type': opt, 'args': {'stepsize': 0.01}}), vocab_size=63)
+
+
+@pytest.mark.parametrize('opt', ['adam', 'sgd'])
+def test_dispatched_loop_matches_local_loop(workload, tmp_path, opt):
+    dims, theta, fc, gts, df, n, table = workload
+    P, iters = 6, 2
+    batch = {'fc_feats': fc, 'gts': gts}
+
+    local = M.EngineMaster(_spec(P, opt), _engine(workload), log_dir=str(tmp_path / 'a'))
+    local.run([batch], max_iterations=iters)
+
+    e_master, e_worker = _engine(workload), _engine(workload)
+    master = M.EngineMaster(_spec(P, opt), e_master, log_dir=str(tmp_path / 'b'))
+    store = T.LocalStore()
+    worker = N.EngineWorker(e_worker, _spec(P, opt), worker_id=1)
+    th = threading.Thread(target=M.run_worker, args=(T.WorkerClient(store), worker),
+                          kwargs=dict(chunk=4, max_tasks=iters), daemon=True)
+    th.start()
+    master.run_dispatched(T.MasterClient(store), [batch] * iters, max_iterations=iters, result_timeout=120)
+    th.join(timeout=120)
+    assert not th.is_alive()
+
+    a64, a32 = local.e.theta()
+    b64, b32 = master.e.theta()
+    assert np.array_equal(a64.numpy(), b64.numpy())
+    assert [r['score_mean'] for r in local.stats] == [r['score_mean'] for r in master.stats]
+    assert local.opt.t == iters == master.opt.t
+
+
+def test_snapshot_roundtrip(workload, tmp_path):
+    P = 4
+    m1 = M.EngineMaster(_spec(P), _engine(workload), log_dir=str(tmp_path))
+    m1.run([{'fc_feats': workload[2], 'gts': workload[3]}], max_iterations=1)
+    import glob
+    info = glob.glob(str(tmp_path / 'snapshot' / 'z_info_e*_i1-*.json'))
+    assert len(info) == 1
+    sd = torch.load(m1.current_model_path(), weights_only=True)
+    assert sd['logit.weight'].dtype == torch.float64          # fp64 master after the first update
+    st = N._load_state(str(tmp_path / 'snapshot' / 'optimizer.tar'))
+    assert st['t'] == 1 and st['dim'] == workload[0].D
+
+
+def test_schedule_curriculum():
+    cfg = C.Config(noise_stdev=0.1, batch_size=8, schedule_start=2, schedule_limit=3, stdev_divisor=2,
+                   bs_multiplier=2)
+    s = M.Schedule(cfg, 4)
+    hits = []
+    for _ in range(8):
+        s.incr_iteration()
+        hits.append(s.schedule_reached)
+    # iteration.py:184-187: reached at it >= start and (it - start) % limit == 0 -> it = 2, 5, 8
+    assert hits == [False, True, False, False, True, False, False, True]
+    assert s.noise_stdev == 0.1 / 8 and s.batch_size == 64 and s.nb_samples_used == 8 + 8 + 16 * 3 + 32 * 3

@@ -168,3 +168,107 @@ def test_adam_matches_reference_golden(golden_dir):
             assert ratio > 0
     finally:
         e.close()
+
+
+def _embed(e, arr, dtype):
+    out = np.zeros(e.D, dtype)
+    out[:arr.size] = arr
+    return out
+
+
+def test_sgd_matches_reference_golden(golden_dir):
+    """Fused SGD form vs the imported reference SGD driven like run_master (tests/golden/sgd.npz)."""
+    import nicnes
+    z = np.load(golden_dir + '/sgd.npz')
+    e = nicnes.Engine(max_batch=8, max_members=1, noise_len=1 << 22)
+    try:
+        n = z['theta0'].size
+        e.set_theta(_embed(e, z['theta0'], np.float32))
+        for k in range(3):
+            gsum = _embed(e, z['grads'][k] * np.float32(2.0), np.float32)
+            ratio = e.sgd_step(torch.from_numpy(gsum).cuda(), 1, float(z['l2coeff']), float(z['stepsize']),
+                               float(z['momentum']))
+            t64, t32 = e.theta()
+            assert np.array_equal(t64.cpu().numpy()[:n], z['thetas'][k]), k
+            assert np.array_equal(t32.cpu().numpy()[:n], z['thetas'][k].astype(np.float32))
+            _, v, t = e.adam_state()
+            assert np.array_equal(v.cpu().numpy()[:n], z['vs'][k]) and t == k + 1
+            assert ratio > 0
+    finally:
+        e.close()
+
+
+def test_optimizer_update_globalg_forms(golden_dir):
+    """Optimizer.update(globalg): fp32 globalg on the first step (adam.npz, host-side -g + l2*theta)
+    and fp64 globalg from the first step (adam_globalg64.npz)."""
+    import nicnes
+    e = nicnes.Engine(max_batch=8, max_members=1, noise_len=1 << 22)
+    try:
+        z = np.load(golden_dir + '/adam.npz')
+        n = z['theta0'].size
+        e.set_theta(_embed(e, z['theta0'], np.float32))
+        theta = z['theta0'].copy()
+        for k in range(3):
+            gg = -z['grads'][k] + float(z['l2coeff']) * theta       # fp32 at k=0, fp64 after (fact 8)
+            e.optimizer_update(_embed(e, gg, gg.dtype), 'adam', stepsize=float(z['stepsize']))
+            theta = e.theta()[0].cpu().numpy()[:n]
+            assert np.array_equal(theta, z['thetas'][k]), k
+        z = np.load(golden_dir + '/adam_globalg64.npz')
+        n = z['theta0'].size
+        e.set_theta(_embed(e, z['theta0'], np.float32))
+        e.set_adam_state(np.zeros(e.D), np.zeros(e.D), 0)
+        for k in range(2):
+            e.optimizer_update(_embed(e, z['globalgs'][k], np.float64), 'adam', stepsize=float(z['stepsize']))
+            assert np.array_equal(e.theta()[0].cpu().numpy()[:n], z['thetas'][k]), k
+    finally:
+        e.close()
+
+
+def test_engine_worker_and_dispatched_master(eng):
+    """EngineWorker.fitness_batch == Engine.evaluate; one dispatched iteration over the in-process
+    transport gives the same theta as the local (PopulationRunner) loop."""
+    import threading
+    import nicnes.synthetic as S
+    from nicnes import config as C, master as M, nes as N, transport as T
+    dims = O.Dims()
+    theta = O.make_theta(dims, 0, 4.0, 0.1)
+    B, P = 16, 8
+    fc = np.random.Generator(np.random.PCG64(1234)).standard_normal((B, dims.F)).astype(np.float32)
+    base, _, _ = O.decode(dims, theta, fc)
+    gts, df, ref_len_raw = S.build_references(base, dims.vocab_size, seed=11, df_sets=256)
+    _load(eng, theta, fc, gts, df, ref_len_raw)
+    exp = {'algorithm': 'nic_nes', 'nb_offspring': P,
+           'config': {'noise_stdev': SIGMA, 'batch_size': B, 'l2coeff': 1e-7, 'snapshot_freq': 0},
+           'policy_options': {'net': 'fc_caption', 'fitness': 'greedy', 'model_options': {}},
+           'optimizer_options': {'type': 'adam', 'args': {'stepsize': 1e-3}}}
+    spec = C.ExperimentSpec(exp)
+    batch = {'fc_feats': fc, 'gts': gts}
+    worker = N.EngineWorker(eng, spec, worker_id=0)
+    res = worker.fitness_batch(0, N.NESTask(batch_data=batch, noise_stdev=SIGMA, iteration=4), 0, P)
+    fit = eng.evaluate(4, 0, P, SIGMA).cpu().numpy()
+    assert np.array_equal(np.stack([r.fitness for r in res]), fit)
+    assert [r.noise_idx for r in res] == [O.noise_index(7, 4, m, NOISE_LEN, dims.D) for m in range(P)]
+
+    eng.set_theta(theta)
+    local = M.EngineMaster(spec, eng)
+    local.run([batch], max_iterations=1)
+    want = eng.theta()[0].cpu().numpy()
+
+    eng.set_theta(theta)
+    eng.set_adam_state(np.zeros(eng.D), np.zeros(eng.D), 0)
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        master = M.EngineMaster(spec, eng, log_dir=d)
+        store = T.LocalStore()
+        # worker and master share one engine here: the worker runs to completion before the master
+        # updates (it only needs the task), so run it synchronously after the task is declared.
+        mc = T.MasterClient(store)
+        orig_declare = mc.declare_task
+
+        def declare_and_work(task):
+            tid = orig_declare(task)
+            M.run_worker(T.WorkerClient(store), N.EngineWorker(eng, spec, worker_id=1), chunk=3, max_tasks=1)
+            return tid
+        mc.declare_task = declare_and_work
+        master.run_dispatched(mc, [batch], max_iterations=1, result_timeout=60)
+    assert np.array_equal(eng.theta()[0].cpu().numpy(), want)

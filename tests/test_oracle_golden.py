@@ -82,6 +82,24 @@ def test_adam_matches_reference(golden_dir):
         assert ratio == pytest.approx(z['ratios'][k], rel=1e-12)
 
 
+def test_sgd_matches_reference(golden_dir):
+    z = np.load(golden_dir + '/sgd.npz')
+    opt = O.SGDOracle(z['theta0'].copy(), float(z['stepsize']), float(z['momentum']))
+    for k in range(3):
+        ratio, theta = O.master_update(opt, z['grads'][k], float(z['l2coeff']))
+        assert np.array_equal(theta, z['thetas'][k]) and np.array_equal(opt.v, z['vs'][k])
+        assert ratio == pytest.approx(z['ratios'][k], rel=1e-12)
+
+
+def test_adam_fp64_globalg_matches_reference(golden_dir):
+    z = np.load(golden_dir + '/adam_globalg64.npz')
+    opt = O.AdamOracle(z['theta0'].copy(), float(z['stepsize']))
+    for k in range(2):
+        _, theta = opt.update(z['globalgs'][k])
+        assert np.array_equal(theta, z['thetas'][k])
+    assert np.array_equal(opt.m, z['m']) and np.array_equal(opt.v, z['v'])
+
+
 def test_centered_ranks_docstring(golden_dir):
     z = np.load(golden_dir + '/ranks.npz')
     assert np.allclose(O.compute_centered_ranks(z['x']), z['y'], atol=1e-8)
