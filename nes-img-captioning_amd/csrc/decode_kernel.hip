@@ -39,6 +39,27 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef DECODE_SCHED
 #define DECODE_SCHED 0
 #endif
+#ifndef DECODE_PROF
+#define DECODE_PROF 0      // timing-only build: per-wave section cycles written over seq (wrong tokens)
+#endif
+#if DECODE_PROF
+#define PROF_STAMP(sec)                                                                          \
+    do {                                                                                         \
+        unsigned long long t_;                                                                   \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                 \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        const uint32_t d_ = (uint32_t)(t_ - prof_t0);                                            \
+        _Pragma("unroll") for (int k_ = 0; k_ < 8; ++k_) prof_acc[k_] += prof_cur == k_ ? d_ : 0u;  \
+        prof_t0 = t_;                                                                            \
+        prof_cur = (sec);                                                                        \
+    } while (0)
+#else
+#define PROF_STAMP(sec) do { } while (0)
+#endif
+#ifndef DECODE_CELL
+#define DECODE_CELL 1      // 1: two-pass cell (i2h partials in lane scratch); 2: fused 64-row stages
+#endif
 
 // ---- buffer helpers ------------------------------------------------------------------------
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
@@ -464,6 +485,12 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
 
     float xB[64], hB[64];
     StageRegs sr;
+#if DECODE_PROF
+    uint32_t prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int prof_cur = 0;
+    unsigned long long prof_t0;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(prof_t0)::"memory");
+#endif
 
     // ========== t = 0: x = img_embed(fc) (nets.py:194-195) ==================================
     {
@@ -501,6 +528,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
     int it = 0;
     bool unfinished = true;
     for (int t = 0; t <= p.T; ++t) {
+        PROF_STAMP(1);
         // ========== x = embed(it) (nets.py:196-199) =========================================
         if (t > 0) {
             const uint32_t eo = 4u * ((uint32_t)p.off_emb_w + (uint32_t)it * 128u + 4u * hh);
@@ -522,8 +550,72 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
         // i2h products into 20 lane-private gate-sum slots (slot 5U+q: gate chunk q, units
         // 32U..32U+31); tiles 20..39 add b_h2h + Wh.h in place, so x and h are never live in
         // registers together; then nn_lstm_cell (the oracle's own function) runs per unit.
-#if !(DECODE_ABLATE & 4)
+#if !(DECODE_ABLATE & 4) && DECODE_CELL == 2
+        // fused form: one 64-row stage = [Wi rows | Wh rows] of gate tile (q, U); the chain
+        // b_i + Wi.x, + b_h, + Wh.h runs in one accumulator, and the gates of a 32-unit block U are
+        // folded as they complete (order g1, g2, i, f, o), so only one running value is held.
         {
+            auto cell_load = [&](int n, Stage64Regs& r) {
+                const int U = n / 5, q = (n % 5 + 3) % 5;        // q order 3, 4, 0, 1, 2
+                const uint32_t rowbase = (uint32_t)(q * 128 + 32 * U);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int f = tid + NTHREADS * u, row = (f >> 5) & 31, q4 = f & 31;
+                    const uint32_t base = u < 2 ? (uint32_t)p.off_i2h_w : (uint32_t)p.off_h2h_w;
+                    const uint32_t off = 4u * (base + (rowbase + (uint32_t)row) * 128u + 4u * (uint32_t)q4);
+                    r.w[u] = ld4(theta_r, off);
+                    r.z[u] = ld4(noise_r, off);
+                }
+                const int br = tid & 63;
+                const uint32_t bbase = br < 32 ? (uint32_t)p.off_i2h_b : (uint32_t)p.off_h2h_b;
+                const uint32_t boff = 4u * (bbase + rowbase + (uint32_t)(br & 31));
+                r.bw = ld1(theta_r, boff);
+                r.bz = ld1(noise_r, boff);
+            };
+            Stage64Regs cr;
+            cell_load(0, cr);
+            stage64_store(lds, 0, 64, sigma, tid, cr);
+            __syncthreads();
+            f32x16 hold;
+            for (int n = 0; n < 20; ++n) {
+                cell_load(min(n + 1, 19), cr);
+                const float* buf = lds + (n & 1) * STAGE64_FLOATS;
+                const float* wsg = buf + sgn * (64 * LDS_ROW);
+                const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * sgn;
+                f32x16 acc = mfma_tile(bias_init(bsg, hh), wsg, xB, lane);
+                acc = acc + bias_init(bsg + 32, hh);
+                if (t > 0) acc = mfma_tile(acc, wsg + 32 * LDS_ROW, hB, lane);   // h = 0 at t = 0
+                const int U = n / 5, j = n % 5;
+                if (j == 0) {                                   // g1
+                    hold = acc;
+                } else if (j == 1) {                            // g = max(g1, g2)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) hold[r] = hold[r] > acc[r] ? hold[r] : acc[r];
+                } else if (j == 2) {                            // ig * g
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) hold[r] = nn_sigmoidf(acc[r]) * hold[r];
+                } else if (j == 3) {                            // c' = f * c + ig * g
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float cold = (t == 0) ? 0.f : ld1(scr_r, lo, C_SLOT(16 * U + r));
+                        const float fc = nn_sigmoidf(acc[r]) * cold;
+                        const float cn = fc + hold[r];
+                        st1(scr_r, lo, C_SLOT(16 * U + r), cn);
+                        hold[r] = cn;
+                    }
+                } else {                                        // h' = o * tanh(c')
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) st1(scr_r, lo, H_SLOT(16 * U + r), nn_sigmoidf(acc[r]) * nn_tanhf(hold[r]));
+                }
+                stage64_store(lds + ((n + 1) & 1) * STAGE64_FLOATS, 0, 64, sigma, tid, cr);
+                __syncthreads();
+            }
+#pragma unroll
+            for (int i = 0; i < 64; ++i) hB[i] = ld1(scr_r, lo, H_SLOT(i));
+        }
+#elif !(DECODE_ABLATE & 4)
+        {
+            PROF_STAMP(2);
             const int ntile = 40;
             auto desc = [&](int n) {
                 const int which = n >= 20, m = n - 20 * which, U = m / 5, q = m % 5;
@@ -546,6 +638,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
                 __syncthreads();
             }
             // pass 2: + b_h2h + Wh.h (x not live)
+            PROF_STAMP(3);
 #pragma unroll
             for (int i = 0; i < 64; ++i) hB[i] = (t == 0) ? 0.f : ld1(scr_r, lo, H_SLOT(i));
             for (int n = 20; n < ntile; ++n) {
@@ -564,6 +657,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
                 __syncthreads();
             }
             // elementwise cell: c' = f*c + i*max(g1,g2), h' = o*tanh(c')
+            PROF_STAMP(4);
             for (int U = 0; U < 4; ++U) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
@@ -603,6 +697,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
             return d;
         };
         const int nst = (p.V1 + 63) >> 6;
+        PROF_STAMP(5);
         RowState st;
         row_state_init(st);
         Stage64Regs s64;
@@ -641,6 +736,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
             prev1 = acc1;
         }
         epilogue64(st, prev0, prev1, 64 * (nst - 1) + 4 * hh);
+        PROF_STAMP(6);
         // merge the two lane halves that share this batch row
         const float m_o = __shfl_xor(st.m, 32);
         const float s_o = __shfl_xor(st.s, 32);
@@ -679,10 +775,17 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
         // finished mask (nets.py:236-243)
         unfinished = unfinished && (tok > 0);
         it = unfinished ? tok : 0;
+#if !DECODE_PROF
         if (hh == 0 && row_valid) p.seq[(((size_t)member * 2 + sgn) * p.B + b) * p.T + (t - 1)] = it;
+#endif
         if (t == p.T) break;
         if (!__syncthreads_or((unfinished && row_valid) ? 1 : 0)) break;
     }
+#if DECODE_PROF
+    PROF_STAMP(7);
+    if (lane == 0 && p.seq && slab == 0)
+        for (int k = 0; k < 8; ++k) p.seq[(size_t)member * 2 * p.B * p.T + wave * 8 + k] = (int32_t)prof_acc[k];
+#endif
 #undef C_SLOT
 #undef H_SLOT
 #undef P_SLOT

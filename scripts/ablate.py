@@ -42,11 +42,20 @@ def main():
             e.evaluate(r + 1, 0, pop, 0.01)
             res[k].append(e.kernel_times()[0])
     ref = engines['base'].evaluate(99, 0, 8, 0.01, return_seq=True)
-    for k in ():
+    for k in [x for x in os.environ.get('EXACT', '').split(',') if x]:   # variants that must match base
         if k in engines:
             got = engines[k].evaluate(99, 0, 8, 0.01, return_seq=True)
             print(k, 'tokens == base:', bool(torch.equal(got[1], ref[1])), 'fitness == base:',
                   bool(torch.equal(got[0], ref[0])))
+    for k in [x for x in engines if x.startswith('prof')]:   # DECODE_PROF builds: section cycles
+        _, seq = engines[k].evaluate(50, 0, pop, 0.01, return_seq=True)
+        cyc = seq.view(pop, -1)[:, :64].reshape(pop, 8, 8).double().cpu().numpy()   # [member, wave, section]
+        names = ['img', 'embed', 'cell_p1', 'cell_p2', 'cell_elem', 'logit', 'finish', 'tail']
+        tot = cyc.sum(axis=2).mean()
+        print(k, 'mean cycles per wave:', json.dumps({n: round(float(cyc[:, :, i].mean()), 0) for i, n in enumerate(names)}),
+              'total', round(float(tot), 0), 'frac', json.dumps({n: round(float(cyc[:, :, i].mean() / tot), 4)
+                                                                   for i, n in enumerate(names)}))
+        print(k, 'sgn0 vs sgn1 logit cycles', float(cyc[:, :4, 5].mean()), float(cyc[:, 4:, 5].mean()))
     base = np.median(res['base'])
     out = {k: {'median_ms': round(float(np.median(v)), 3), 'min_ms': round(float(np.min(v)), 3),
                'vs_base': round(float(np.median(v) / base), 3)} for k, v in res.items()}
