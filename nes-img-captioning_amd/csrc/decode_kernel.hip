@@ -50,7 +50,7 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                 \
         __builtin_amdgcn_sched_barrier(0);                                                       \
         const uint32_t d_ = (uint32_t)(t_ - prof_t0);                                            \
-        _Pragma("unroll") for (int k_ = 0; k_ < 8; ++k_) prof_acc[k_] += prof_cur == k_ ? d_ : 0u;  \
+        _Pragma("unroll") for (int k_ = 0; k_ < 16; ++k_) prof_acc[k_] += prof_cur == k_ ? d_ : 0u;  \
         prof_t0 = t_;                                                                            \
         prof_cur = (sec);                                                                        \
     } while (0)
@@ -60,6 +60,15 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef DECODE_CELL
 #define DECODE_CELL 1      // 1: two-pass cell (i2h partials in lane scratch); 2: fused 64-row stages
 #endif
+
+// lane id recomputed at the point of use (volatile: never hoisted or kept live across the logit
+// loop), so lane-derived LDS / buffer offsets are cheap VALU instead of registers the compiler
+// would spill and reload behind the in-flight staging loads (vmcnt is in-order)
+__device__ __forceinline__ int lane_fresh() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 
 // ---- buffer helpers ------------------------------------------------------------------------
 __device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes) {
@@ -347,18 +356,24 @@ struct Stage64Regs {
     float bw, bz;
 };
 
+__device__ __forceinline__ f32x4 ld4s(rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+}
+
+// thread tid loads floats 4*tid + 2048*u .. +3 of the stage (row (tid>>5) + 16u, k 4*(tid&31)):
+// one lane offset (16*tid) for every load, the stage / chunk offsets ride in the scalar offset
 __device__ __forceinline__ void stage64_load(rsrc_t lw, rsrc_t lz, rsrc_t lbw, rsrc_t lbz, int s, int tid,
                                              Stage64Regs& r) {
+    const uint32_t vo = 16u * (uint32_t)tid;
+    const uint32_t so = 32768u * (uint32_t)s;
+    const uint32_t vb = (vo >> 2) & 252u;               // 4 * (tid & 63), recomputed, never spilled
+    r.bw = ld1(lbw, vb, 256u * (uint32_t)s);
+    r.bz = ld1(lbz, vb, 256u * (uint32_t)s);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int f = tid + NTHREADS * u, row = f >> 5, q = f & 31;
-        const uint32_t off = 4u * (uint32_t)((64 * s + row) * 128 + 4 * q);
-        r.w[u] = ld4(lw, off);
-        r.z[u] = ld4(lz, off);
+        r.w[u] = ld4s(lw, vo, so + 8192u * u);
+        r.z[u] = ld4s(lz, vo, so + 8192u * u);
     }
-    const uint32_t boff = 4u * (uint32_t)(64 * s + (tid & 63));
-    r.bw = ld1(lbw, boff);
-    r.bz = ld1(lbz, boff);
 }
 
 __device__ __forceinline__ void stage64_store(float* buf, int s, int V1, float sigma, int tid, const Stage64Regs& r) {
@@ -486,7 +501,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
     float xB[64], hB[64];
     StageRegs sr;
 #if DECODE_PROF
-    uint32_t prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t prof_acc[16] = {0};
     int prof_cur = 0;
     unsigned long long prof_t0;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(prof_t0)::"memory");
@@ -643,12 +658,15 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
             for (int i = 0; i < 64; ++i) hB[i] = (t == 0) ? 0.f : ld1(scr_r, lo, H_SLOT(i));
             for (int n = 20; n < ntile; ++n) {
                 const int nn = min(n + 1, ntile - 1);
-                stage_load(theta_r, noise_r, desc(nn), tid, sr);
-                const float* buf = lds + (n & 1) * STAGE_FLOATS;
                 const int m = n - 20;
+                // partials first: vmcnt is in-order, so loads issued after the staging loads
+                // would wait for them
                 f32x16 acc;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = ld1(scr_r, lo, P_SLOT(16 * m + r));
+                __builtin_amdgcn_sched_barrier(0);
+                stage_load(theta_r, noise_r, desc(nn), tid, sr);
+                const float* buf = lds + (n & 1) * STAGE_FLOATS;
                 acc = acc + bias_init(buf + 2 * SIGN_FLOATS + 32 * sgn, hh);
                 if (t > 0) acc = mfma_tile(acc, buf + sgn * SIGN_FLOATS, hB, lane);   // h = 0 at t = 0
 #pragma unroll
@@ -708,29 +726,44 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
 #pragma unroll
         for (int r = 0; r < 16; ++r) { prev0[r] = NEG_INF; prev1[r] = NEG_INF; }
         for (int s = 0; s < nst; ++s) {
+#if DECODE_PROF >= 2
+            PROF_STAMP(8);
+#endif
 #if !(DECODE_ABLATE & 2)
-            stage64_load(lw_r, lz_r, lbw_r, lbz_r, min(s + 1, nst - 1), tid, s64);
+            stage64_load(lw_r, lz_r, lbw_r, lbz_r, min(s + 1, nst - 1), wave * 64 + lane_fresh(), s64);
+#endif
+#if DECODE_PROF >= 2
+            PROF_STAMP(9);
 #endif
             const float* buf = lds + (s & 1) * STAGE64_FLOATS;
             const float* wsg = buf + sgn * (64 * LDS_ROW);
             const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * sgn;
             f32x16 acc0, acc1;
             if (sgn == 0) {
-                mfma_stage64(wsg, bsg, hB, lane, acc0, acc1);
+                mfma_stage64(wsg, bsg, hB, lane_fresh(), acc0, acc1);
 #if !(DECODE_ABLATE & 1)
-                epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * hh);
+                epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
 #endif
             } else {
 #if !(DECODE_ABLATE & 1)
-                epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * hh);
+                epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
 #endif
-                mfma_stage64(wsg, bsg, hB, lane, acc0, acc1);
+                mfma_stage64(wsg, bsg, hB, lane_fresh(), acc0, acc1);
             }
+#if DECODE_PROF >= 2
+            PROF_STAMP(10);
+#endif
 #if !(DECODE_ABLATE & 2)
-            stage64_store(lds + ((s + 1) & 1) * STAGE64_FLOATS, min(s + 1, nst - 1), p.V1, sigma, tid, s64);
+            stage64_store(lds + ((s + 1) & 1) * STAGE64_FLOATS, min(s + 1, nst - 1), p.V1, sigma, wave * 64 + lane_fresh(), s64);
+#endif
+#if DECODE_PROF >= 2
+            PROF_STAMP(11);
 #endif
 #if !(DECODE_ABLATE & 8)
             __syncthreads();
+#endif
+#if DECODE_PROF >= 2
+            PROF_STAMP(5);
 #endif
             prev0 = acc0;
             prev1 = acc1;
@@ -784,7 +817,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
 #if DECODE_PROF
     PROF_STAMP(7);
     if (lane == 0 && p.seq && slab == 0)
-        for (int k = 0; k < 8; ++k) p.seq[(size_t)member * 2 * p.B * p.T + wave * 8 + k] = (int32_t)prof_acc[k];
+        for (int k = 0; k < 16; ++k) p.seq[(size_t)member * 2 * p.B * p.T + wave * 16 + k] = (int32_t)prof_acc[k];
 #endif
 #undef C_SLOT
 #undef H_SLOT
