@@ -75,7 +75,8 @@ int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t
 
 /* Fixed document-frequency table (CiderD(df='coco-train-idxs'), src/captioning/policies.py:72):
  * sorted packed n-gram keys (n<<56 | t0<<42 | t1<<28 | t2<<14 | t3), df counts, and
- * ref_len = log(raw ref_len) as the scorer uses it. */
+ * ref_len = log(raw ref_len) as the scorer uses it. The engine keeps its own hashed copy, built
+ * here (synchronising); the caller's arrays are borrowed as for every nicnes_set_* call. */
 int nicnes_set_df_table(nicnes_handle* h, const uint64_t* keys, const double* df, int64_t n, double ref_len_log);
 
 /* Noise-table offsets of members [member_begin, member_begin + count) at `iteration`. */

@@ -7,6 +7,9 @@ struct CiderTables {
     const uint64_t* df_keys;   // sorted packed n-gram keys of the document-frequency table
     const double* df_vals;     // document frequency per key
     int64_t df_n;
+    const uint64_t* hash_keys; // open-addressing copy of the df table (0 = empty slot; no valid key is 0)
+    const double* hash_vals;
+    uint64_t hash_mask;        // capacity - 1 (capacity a power of two >= 2 df_n)
     double ref_len;            // log(ref_len_raw)  (CiderScorer fixed-df mode)
     // per-reference vectors (written by nicnes_cook_refs_kernel)
     uint64_t* ref_keys;        // [n_refs, 64] distinct n-grams
@@ -16,6 +19,9 @@ struct CiderTables {
     double* ref_norm;          // [n_refs, 4]
 };
 
+extern "C" uint64_t nicnes_df_hash_capacity(int64_t n);
+extern "C" hipError_t nicnes_launch_df_hash_build(const uint64_t* keys, const double* vals, int64_t n, uint64_t* hkeys,
+                                                  double* hvals, uint64_t mask, hipStream_t stream);
 extern "C" hipError_t nicnes_launch_cook_refs(const int32_t* ref_tokens, int n_refs, int T, const CiderTables* tb,
                                               hipStream_t stream);
 extern "C" hipError_t nicnes_launch_cider(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,

@@ -17,11 +17,11 @@
 
 #define REF_SLOTS 64
 
+// lane j owns n-gram slot i = j & 15 of size n = (j >> 4) + 1: one 16-lane segment per n, so
+// per-n sums are 4-step segmented reductions
 __device__ __forceinline__ void slot_of_lane(int j, int& n, int& i) {
-    if (j < 16) { n = 1; i = j; }
-    else if (j < 31) { n = 2; i = j - 16; }
-    else if (j < 45) { n = 3; i = j - 31; }
-    else { n = 4; i = j - 45; }           // lanes 58..63: i >= 13, never valid for T = 16
+    n = (j >> 4) + 1;
+    i = j & 15;
 }
 
 // length of array_to_str(row): tokens up to and including the first 0
@@ -37,13 +37,49 @@ __device__ __forceinline__ uint64_t pack_ngram(const int32_t* row, int n, int i)
     return key;
 }
 
-__device__ __forceinline__ double df_lookup(const uint64_t* keys, const double* vals, int64_t n, uint64_t key) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (keys[mid] < key) lo = mid + 1; else hi = mid;
+__device__ __host__ __forceinline__ uint64_t df_hash(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+// df of an n-gram: linear probing in the hash copy of the sorted table (0 when absent)
+__device__ __forceinline__ double df_lookup(const CiderTables& tb, uint64_t key) {
+    uint64_t h = df_hash(key) & tb.hash_mask;
+    for (uint64_t probe = 0; probe <= tb.hash_mask; ++probe) {
+        const uint64_t k = tb.hash_keys[h];
+        if (k == key) return tb.hash_vals[h];
+        if (k == 0ull) return 0.0;
+        h = (h + 1) & tb.hash_mask;
     }
-    return (lo < n && keys[lo] == key) ? vals[lo] : 0.0;
+    return 0.0;
+}
+
+__global__ __launch_bounds__(256) void nicnes_df_hash_build_kernel(const uint64_t* keys, const double* vals, int64_t n,
+                                                                   unsigned long long* hkeys, double* hvals,
+                                                                   uint64_t mask) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long key = keys[i];
+    uint64_t h = df_hash(key) & mask;
+    for (uint64_t probe = 0; probe <= mask; ++probe) {
+        const unsigned long long prev = atomicCAS(&hkeys[h], 0ull, key);
+        if (prev == 0ull || prev == key) {
+            hvals[h] = vals[i];
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
+// sum over the lane's 16-lane segment (every lane of the segment gets it)
+__device__ __forceinline__ double seg_sum(double v) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o);
+    return v;
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -65,22 +101,22 @@ __device__ __forceinline__ NgramLane ngram_lane(const int32_t* row, int T, int l
     const int L = caption_len(row, T);
     int i;
     slot_of_lane(lane, g.n, i);
-    g.valid = (lane < 58) && (i + g.n <= L);
+    g.valid = i + g.n <= L;
     g.key = g.valid ? pack_ngram(row, g.n, i) : 0ull;
     int tf = 0;
     bool first = g.valid;
-    for (int o = 0; o < 64; ++o) {
-        const uint64_t k2 = __shfl(g.key, o);
-        const bool v2 = __shfl((int)g.valid, o) != 0;
-        if (g.valid && v2 && k2 == g.key) {
+    const int seg = lane & 48;
+    for (int o = 0; o < 16; ++o) {             // equal keys have equal n: same segment
+        const uint64_t k2 = __shfl(g.key, seg | o);
+        if (g.valid && k2 == g.key) {           // invalid lanes hold key 0, never a valid key
             ++tf;
-            if (o < lane) first = false;
+            if ((seg | o) < lane) first = false;
         }
     }
     g.first = first;
     g.vec = 0.0;
     if (first) {
-        const double df = df_lookup(tb.df_keys, tb.df_vals, tb.df_n, g.key);
+        const double df = df_lookup(tb, g.key);
         g.vec = (double)tf * (tb.ref_len - log(df > 1.0 ? df : 1.0));
     }
     return g;
@@ -100,15 +136,12 @@ __global__ __launch_bounds__(256) void nicnes_cook_refs_kernel(const int32_t* re
         tb.ref_keys[(size_t)r * REF_SLOTS + rank] = g.key;
         tb.ref_vec[(size_t)r * REF_SLOTS + rank] = g.vec;
     }
-    double nrm[4];
-#pragma unroll
-    for (int n = 1; n <= 4; ++n) nrm[n - 1] = sqrt(wave_sum((g.first && g.n == n) ? g.vec * g.vec : 0.0));
+    const double nrm = sqrt(seg_sum(g.first ? g.vec * g.vec : 0.0));     // norm of this lane's n
+    if ((lane & 15) == 0) tb.ref_norm[(size_t)r * 4 + (lane >> 4)] = nrm;
     if (lane == 0) {
         tb.ref_count[r] = __popcll(firsts);
         const int L = caption_len(row, T);
         tb.ref_len2[r] = L > 1 ? L - 1 : 0;          // bigram count (counts2vec 'length' quirk)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) tb.ref_norm[(size_t)r * 4 + n] = nrm[n];
     }
 }
 
@@ -122,12 +155,10 @@ __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, i
     for (int b = wave; b < B; b += 4) {
         const int32_t* row = seq + ((size_t)cand * B + b) * T;
         const NgramLane g = ngram_lane(row, T, lane, tb);
-        double nh[4];
-#pragma unroll
-        for (int n = 1; n <= 4; ++n) nh[n - 1] = sqrt(wave_sum((g.first && g.n == n) ? g.vec * g.vec : 0.0));
+        const double nh = sqrt(seg_sum(g.first ? g.vec * g.vec : 0.0));   // |vec_hyp[n]| for this lane's n
         const int L = caption_len(row, T);
         const int len_h = L > 1 ? L - 1 : 0;
-        double score[4] = {0.0, 0.0, 0.0, 0.0};
+        double score = 0.0;                                                  // score[n] of this segment
         const int r0 = img_ref_start[b], r1 = img_ref_start[b + 1];
         for (int r = r0; r < r1; ++r) {
             // vr[g] for this lane's n-gram (0 when the ref lacks it)
@@ -140,16 +171,16 @@ __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, i
             const double contrib = g.first ? (g.vec < vr ? g.vec : vr) * vr : 0.0;
             const double delta = (double)(len_h - tb.ref_len2[r]);
             const double pen = exp(-(delta * delta) / sigma2x2);
-#pragma unroll
-            for (int n = 1; n <= 4; ++n) {
-                double val = wave_sum(g.n == n ? contrib : 0.0);
-                const double nr = tb.ref_norm[(size_t)r * 4 + n - 1];
-                if (nh[n - 1] != 0.0 && nr != 0.0) val /= (nh[n - 1] * nr);
-                score[n - 1] += val * pen;
-            }
+            double val = seg_sum(contrib);
+            const double nr = tb.ref_norm[(size_t)r * 4 + (lane >> 4)];
+            if (nh != 0.0 && nr != 0.0) val /= (nh * nr);
+            score += val * pen;
         }
+        // (score[0] + score[1]) + (score[2] + score[3]) across the four segments
+        score += __shfl_xor(score, 16);
+        score += __shfl_xor(score, 32);
         if (lane == 0) {
-            double avg = (score[0] + score[1] + score[2] + score[3]) / 4.0;
+            double avg = score / 4.0;
             avg /= (double)(r1 - r0);
             avg *= 10.0;
             row_score[b] = avg;
@@ -161,6 +192,20 @@ __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, i
         for (int b = 0; b < B; ++b) s += row_score[b];
         fitness_out[cand] = (s / (double)B) * 100.0;        // float(cider * 100), policies.py:125
     }
+}
+
+extern "C" uint64_t nicnes_df_hash_capacity(int64_t n) {
+    uint64_t c = 64;
+    while (c < 2ull * (uint64_t)n) c <<= 1;
+    return c;
+}
+
+extern "C" hipError_t nicnes_launch_df_hash_build(const uint64_t* keys, const double* vals, int64_t n, uint64_t* hkeys,
+                                                  double* hvals, uint64_t mask, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(nicnes_df_hash_build_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, keys, vals, n,
+                       (unsigned long long*)hkeys, hvals, mask);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t nicnes_launch_cook_refs(const int32_t* ref_tokens, int n_refs, int T, const CiderTables* tb,

@@ -57,8 +57,11 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #else
 #define PROF_STAMP(sec) do { } while (0)
 #endif
+#ifndef DECODE_IEPI
+#define DECODE_IEPI 0      // 1: logit epilogue folded into the MFMA stream of each wave (no sign stagger)
+#endif
 #ifndef DECODE_CELL
-#define DECODE_CELL 1      // 1: two-pass cell (i2h partials in lane scratch); 2: fused 64-row stages
+#define DECODE_CELL 1      // 1: two-pass cell, 32-row tiles; 2: fused single pass; 3: two-pass, 64-row stages, folded gates
 #endif
 
 // lane id recomputed at the point of use (volatile: never hoisted or kept live across the logit
@@ -359,6 +362,16 @@ struct Stage64Regs {
 __device__ __forceinline__ f32x4 ld4s(rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
 }
+#ifndef LOGIT_Z_AUX
+#define LOGIT_Z_AUX 0      // cache policy of the member's noise-slice loads in the logit stages
+#endif
+#ifndef LOGIT_W_AUX
+#define LOGIT_W_AUX 0
+#endif
+template <int AUX>
+__device__ __forceinline__ f32x4 ld4p(rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, AUX));
+}
 
 // thread tid loads floats 4*tid + 2048*u .. +3 of the stage (row (tid>>5) + 16u, k 4*(tid&31)):
 // one lane offset (16*tid) for every load, the stage / chunk offsets ride in the scalar offset
@@ -371,8 +384,8 @@ __device__ __forceinline__ void stage64_load(rsrc_t lw, rsrc_t lz, rsrc_t lbw, r
     r.bz = ld1(lbz, vb, 256u * (uint32_t)s);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        r.w[u] = ld4s(lw, vo, so + 8192u * u);
-        r.z[u] = ld4s(lz, vo, so + 8192u * u);
+        r.w[u] = ld4p<LOGIT_W_AUX>(lw, vo, so + 8192u * u);
+        r.z[u] = ld4p<LOGIT_Z_AUX>(lz, vo, so + 8192u * u);
     }
 }
 
@@ -406,6 +419,159 @@ __device__ __forceinline__ void mfma_stage64(const float* w, const float* bias, 
         for (int c = 0; c < 4; ++c) {
             a0[c] = *reinterpret_cast<const f32x4*>(row0 + T * 32 + 4 * c);
             a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bop[16 * T + jj], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
+        }
+    }
+}
+
+// the same two chains continuing from given accumulators (no bias initialisation)
+__device__ __forceinline__ void mfma_stage64_acc(const float* w, const float (&Bop)[64], int lane, f32x16& acc0,
+                                                 f32x16& acc1) {
+    const int hh = lane >> 5;
+    const float* row0 = w + (lane & 31) * LDS_ROW + hh * 16;
+    const float* row1 = row0 + 32 * LDS_ROW;
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+        f32x4 a0[4], a1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            a0[c] = *reinterpret_cast<const f32x4*>(row0 + T * 32 + 4 * c);
+            a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bop[16 * T + jj], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
+        }
+    }
+}
+
+// ---- logit stages staged by LDS-DMA (DECODE_GLDS) ----------------------------------------------
+// One stage buffer: region 0 = 64 rows x 128 (raw w, then W+), region 1 (raw z, then W-), then
+// bias+ (64) | bias- (64). Rows are unpadded; 16-byte chunk `pre` of row r sits at chunk
+// pre ^ (r & 15) (conflict-free A reads). The DMA writes lane-linearly, so the permutation is on
+// the per-lane SOURCE offset. Each lane later reads back exactly the chunks its own DMA wrote and
+// forms W+/W- in place: no registers carry the stage across the MFMA phase.
+#define GST_FLOATS (2 * 64 * 128 + 128)
+#ifndef DECODE_GLDS
+#define DECODE_GLDS 0
+#endif
+typedef __attribute__((address_space(3))) void* lds_vptr;
+
+__device__ __forceinline__ uint32_t glds_src_off(int j, int lane) {
+    const int row = 2 * j + (lane >> 5), pos = lane & 31, pre = pos ^ (row & 15);
+    const int q = 8 * (pre >> 3) + 2 * (pre & 3) + ((pre >> 2) & 1);      // natural 4-float chunk
+    return 4u * (uint32_t)(row * 128 + 4 * q);
+}
+
+__device__ __forceinline__ void glds_issue(rsrc_t lw, rsrc_t lz, rsrc_t lbw, rsrc_t lbz, float* buf, int s, int wave) {
+    const int lane = lane_fresh();
+    const uint32_t so = 32768u * (uint32_t)s;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int j = 4 * wave + u;
+        const uint32_t vo = glds_src_off(j, lane);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(lw, (lds_vptr)(buf + 256 * j), 16, vo, so, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(lz, (lds_vptr)(buf + 64 * 128 + 256 * j), 16, vo, so, 0, 0);
+    }
+    if (wave == 0) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(lbw, (lds_vptr)(buf + 2 * 64 * 128), 4, 4u * (uint32_t)lane, 256u * (uint32_t)s, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(lbz, (lds_vptr)(buf + 2 * 64 * 128 + 64), 4, 4u * (uint32_t)lane, 256u * (uint32_t)s, 0, 0);
+    }
+}
+
+// after this wave's DMAs landed: W+ = fp32(w + fp32(sigma z)), W- = fp32(w - fp32(sigma z)) in place
+__device__ __forceinline__ void glds_form(float* buf, int s, int V1, float sigma, int wave) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int lane = lane_fresh();
+    float* pw = buf + 256 * (4 * wave) + 4 * lane;
+    f32x4 w[4], z[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {                                  // all reads first: one LDS round trip
+        w[u] = *reinterpret_cast<const f32x4*>(pw + 256 * u);
+        z[u] = *reinterpret_cast<const f32x4*>(pw + 256 * u + 64 * 128);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const f32x4 delta = sigma * z[u];                           // nets.py:102
+        *reinterpret_cast<f32x4*>(pw + 256 * u) = w[u] + delta;    // nets.py:113
+        *reinterpret_cast<f32x4*>(pw + 256 * u + 64 * 128) = w[u] - delta;   // nic_nes_worker.py:151
+    }
+    if (wave == 0) {
+        float* pb = buf + 2 * 64 * 128 + lane;
+        const float bw = pb[0], bz = pb[64];
+        const float delta = sigma * bz;
+        const bool ok = 64 * s + lane < V1;
+        pb[0] = ok ? bw + delta : NEG_INF;
+        pb[64] = ok ? bw - delta : NEG_INF;
+    }
+}
+
+// general stage of two 32-row tiles of a [*, 128] matrix: stage rows 0..31 = matrix rows ra..,
+// 32..63 = rb.. (waves 0-3 stage tile a, waves 4-7 tile b); w_r / z_r address the matrix (base +
+// byte soffset `mat`), b_r / bz_r its bias vector (element offset `bofs`)
+__device__ __forceinline__ void glds_issue2(rsrc_t w_r, rsrc_t z_r, rsrc_t b_r, rsrc_t bz_r, uint32_t mat, uint32_t bofs,
+                                            float* buf, uint32_t ra, uint32_t rb, int wave) {
+    const int lane = lane_fresh();
+    const uint32_t so = mat + 512u * (wave < 4 ? ra : rb);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int j = 4 * wave + u;
+        const uint32_t vo = glds_src_off(j & 15, lane);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(w_r, (lds_vptr)(buf + 256 * j), 16, vo, so, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(z_r, (lds_vptr)(buf + 64 * 128 + 256 * j), 16, vo, so, 0, 0);
+    }
+    if (wave == 0) {
+        const uint32_t rm = min(ra, rb);
+        const uint32_t vb = 4u * ((lane < 32 ? ra - rm : rb - rm) + (uint32_t)(lane & 31));
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_r, (lds_vptr)(buf + 2 * 64 * 128), 4, vb, 4u * (bofs + rm), 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(bz_r, (lds_vptr)(buf + 2 * 64 * 128 + 64), 4, vb, 4u * (bofs + rm), 0, 0);
+    }
+}
+
+// the same two chains continuing from given accumulators (DMA-staged layout)
+__device__ __forceinline__ void mfma_stage64_g_acc(const float* region, const float (&Bop)[64], int lane, f32x16& acc0,
+                                                   f32x16& acc1) {
+    const int r = lane & 31, hh = lane >> 5;
+    const uint32_t lb = (uint32_t)(r * 512) | (uint32_t)(16 * ((4 * hh) ^ (r & 15)));
+    const char* base = reinterpret_cast<const char*>(region);
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+        f32x4 a0[4], a1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t o = lb ^ (uint32_t)(128 * T + 16 * c);
+            a0[c] = *reinterpret_cast<const f32x4*>(base + o);
+            a1[c] = *reinterpret_cast<const f32x4*>(base + o + 32 * 512);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bop[16 * T + jj], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
+        }
+    }
+}
+
+// two chains over one sign region of a DMA-staged stage (swizzled chunk reads)
+__device__ __forceinline__ void mfma_stage64_g(const float* region, const float* bias, const float (&Bop)[64], int lane,
+                                               f32x16& acc0, f32x16& acc1) {
+    const int r = lane & 31, hh = lane >> 5;
+    const uint32_t lb = (uint32_t)(r * 512) | (uint32_t)(16 * ((4 * hh) ^ (r & 15)));   // bytes
+    const char* base = reinterpret_cast<const char*>(region);
+    acc0 = bias_init(bias, hh);
+    acc1 = bias_init(bias + 32, hh);
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+        f32x4 a0[4], a1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t o = lb ^ (uint32_t)(128 * T + 16 * c);
+            a0[c] = *reinterpret_cast<const f32x4*>(base + o);
+            a1[c] = *reinterpret_cast<const f32x4*>(base + o + 32 * 512);
         }
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) {
@@ -450,6 +616,62 @@ __device__ __forceinline__ void epilogue64(RowState& st, const f32x16& P0, const
     st.s = s;
     st.m = mnew;
     if (__any(tmax > st.r1v)) {
+        records16(st, P0, vbase);
+        records16(st, P1, vbase + 32);
+    }
+}
+
+// online-softmax piece over 8 of the previous stage's logits (chunk T: rows 4T..4T+3 of P0, P1)
+__device__ __forceinline__ void softmax_piece(RowState& st, const f32x16& P0, const f32x16& P1, int T) {
+    const float t0 = fmaxf(fmaxf(P0[4 * T], P0[4 * T + 1]), fmaxf(P0[4 * T + 2], P0[4 * T + 3]));
+    const float t1 = fmaxf(fmaxf(P1[4 * T], P1[4 * T + 1]), fmaxf(P1[4 * T + 2], P1[4 * T + 3]));
+    const float mnew = fmaxf(st.m, fmaxf(t0, t1));
+    const float ml = mnew * LOG2E;
+    float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(P0[4 * T + r], LOG2E, -ml));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(P1[4 * T + r], LOG2E, -ml));
+    st.s = s;
+    st.m = mnew;
+}
+
+// the stage's two MFMA chains with the previous stage's softmax folded in between them (one
+// piece per 32-k sub-chunk), so the epilogue VALU issues inside this wave's own MFMA stream;
+// the (rare) record scan follows the chains
+__device__ __forceinline__ void mfma_stage64_iepi(const float* w, const float* bias, const float (&Bop)[64], int lane,
+                                                  f32x16& acc0, f32x16& acc1, RowState& st, const f32x16& P0,
+                                                  const f32x16& P1, int vbase) {
+    const int hh = lane >> 5;
+    const float* row0 = w + (lane & 31) * LDS_ROW + hh * 16;
+    const float* row1 = row0 + 32 * LDS_ROW;
+    acc0 = bias_init(bias, hh);
+    acc1 = bias_init(bias + 32, hh);
+    const float m_before = st.r1v;
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+        f32x4 a0[4], a1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            a0[c] = *reinterpret_cast<const f32x4*>(row0 + T * 32 + 4 * c);
+            a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bop[16 * T + jj], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
+        }
+        softmax_piece(st, P0, P1, T);
+#if DECODE_IEPI >= 2
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);      // A fragments
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // 4 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // ~4 VALU of the piece
+        }
+#endif
+    }
+    if (__any(st.m > m_before)) {            // a new running maximum: scan the records
         records16(st, P0, vbase);
         records16(st, P1, vbase + 32);
     }
@@ -628,6 +850,228 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
 #pragma unroll
             for (int i = 0; i < 64; ++i) hB[i] = ld1(scr_r, lo, H_SLOT(i));
         }
+#elif !(DECODE_ABLATE & 4) && DECODE_CELL == 4
+        // cell 3's two passes, with every stage brought in by LDS-DMA and formed in place
+        {
+            PROF_STAMP(2);
+            auto tile_q = [](int m) { const int j = m % 5; return j < 2 ? j + 3 : j - 2; };   // 3,4,0,1,2
+            auto rows_of = [&](int j, uint32_t& ra, uint32_t& rb) {
+                const int ma = 2 * j, mb = 2 * j + 1;
+                ra = (uint32_t)(tile_q(ma) * 128 + 32 * (ma / 5));
+                rb = (uint32_t)(tile_q(mb) * 128 + 32 * (mb / 5));
+            };
+            auto issue = [&](uint32_t w_off, uint32_t b_off, int j, float* buf) {
+                uint32_t ra, rb;
+                rows_of(j, ra, rb);
+                glds_issue2(theta_r, noise_r, theta_r, noise_r, 4u * w_off, b_off, buf, ra, rb, wave);
+            };
+            // ---- pass 1: b_i + Wi.x -> lane scratch
+            issue((uint32_t)p.off_i2h_w, (uint32_t)p.off_i2h_b, 0, lds);
+            glds_form(lds, 0, 64, sigma, wave);
+            __syncthreads();
+            for (int j = 0; j < 10; ++j) {
+                float* nbuf = lds + ((j + 1) & 1) * GST_FLOATS;
+                if (j < 9) issue((uint32_t)p.off_i2h_w, (uint32_t)p.off_i2h_b, j + 1, nbuf);
+                const float* buf = lds + (j & 1) * GST_FLOATS;
+                f32x16 a0, a1;
+                mfma_stage64_g(buf + sgn * (64 * 128), buf + 2 * 64 * 128 + 64 * sgn, xB, lane_fresh(), a0, a1);
+                const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
+                const int qa = tile_q(2 * j), qb = tile_q(2 * j + 1), ua = (2 * j) / 5, ub = (2 * j + 1) / 5;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) st1(scr_r, lo_, P_SLOT(16 * (5 * ua + qa) + r), a0[r]);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) st1(scr_r, lo_, P_SLOT(16 * (5 * ub + qb) + r), a1[r]);
+                if (j < 9) glds_form(nbuf, 0, 64, sigma, wave);
+                __syncthreads();
+            }
+            PROF_STAMP(3);
+            // ---- pass 2: + b_h + Wh.h, folded per unit block
+#pragma unroll
+            for (int i = 0; i < 64; ++i) hB[i] = (t == 0) ? 0.f : ld1(scr_r, lo, H_SLOT(i));
+            issue((uint32_t)p.off_h2h_w, (uint32_t)p.off_h2h_b, 0, lds);
+            glds_form(lds, 0, 64, sigma, wave);
+            __syncthreads();
+            f32x16 hold;
+            auto fold = [&](int m, const f32x16& acc, uint32_t lo_) {
+                const int U = m / 5, j5 = m % 5;
+                if (j5 == 0) {                                   // g1
+                    hold = acc;
+                } else if (j5 == 1) {                            // g = max(g1, g2)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) hold[r] = hold[r] > acc[r] ? hold[r] : acc[r];
+                } else if (j5 == 2) {                            // ig * g
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) hold[r] = nn_sigmoidf(acc[r]) * hold[r];
+                } else if (j5 == 3) {                            // c' = f * c + ig * g
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float cold = (t == 0) ? 0.f : ld1(scr_r, lo_, C_SLOT(16 * U + r));
+                        const float fcv = nn_sigmoidf(acc[r]) * cold;
+                        const float cn = fcv + hold[r];
+                        st1(scr_r, lo_, C_SLOT(16 * U + r), cn);
+                        hold[r] = cn;
+                    }
+                } else {                                         // h' = o * tanh(c')
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        st1(scr_r, lo_, H_SLOT(16 * U + r), nn_sigmoidf(acc[r]) * nn_tanhf(hold[r]));
+                }
+            };
+            for (int j = 0; j < 10; ++j) {
+                const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
+                const int ma = 2 * j, mb = 2 * j + 1;
+                // scratch partials (and c) are ordinary loads: take them before this stage's DMA
+                // is issued, so their waits do not drain it
+                f32x16 a0, a1, cpre;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) a0[r] = ld1(scr_r, lo_, P_SLOT(16 * (5 * (ma / 5) + tile_q(ma)) + r));
+#pragma unroll
+                for (int r = 0; r < 16; ++r) a1[r] = ld1(scr_r, lo_, P_SLOT(16 * (5 * (mb / 5) + tile_q(mb)) + r));
+                const int mf = (ma % 5 == 3) ? ma : mb;          // the f gate of this stage, if any
+                const bool has_f = (ma % 5 == 3) || (mb % 5 == 3);
+                if (has_f && t > 0) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) cpre[r] = ld1(scr_r, lo_, C_SLOT(16 * (mf / 5) + r));
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                float* nbuf = lds + ((j + 1) & 1) * GST_FLOATS;
+                if (j < 9) issue((uint32_t)p.off_h2h_w, (uint32_t)p.off_h2h_b, j + 1, nbuf);
+                const float* buf = lds + (j & 1) * GST_FLOATS;
+                const float* bsg = buf + 2 * 64 * 128 + 64 * sgn;
+                const int hh_ = lane_fresh() >> 5;
+                a0 = a0 + bias_init(bsg, hh_);
+                a1 = a1 + bias_init(bsg + 32, hh_);
+                if (t > 0) mfma_stage64_g_acc(buf + sgn * (64 * 128), hB, lane_fresh(), a0, a1);   // h = 0 at t = 0
+                // fold (c for the f gate comes from cpre, not a load behind the DMA)
+                auto fold2 = [&](int m, const f32x16& acc) {
+                    if (m % 5 == 3) {
+                        const int U = m / 5;
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const float cold = (t == 0) ? 0.f : cpre[r];
+                            const float fcv = nn_sigmoidf(acc[r]) * cold;
+                            const float cn = fcv + hold[r];
+                            st1(scr_r, lo_, C_SLOT(16 * U + r), cn);
+                            hold[r] = cn;
+                        }
+                    } else {
+                        fold(m, acc, lo_);
+                    }
+                };
+                fold2(ma, a0);
+                fold2(mb, a1);
+                if (j < 9) glds_form(nbuf, 0, 64, sigma, wave);
+                __syncthreads();
+            }
+            PROF_STAMP(4);
+#pragma unroll
+            for (int i = 0; i < 64; ++i) hB[i] = ld1(scr_r, lo, H_SLOT(i));
+        }
+#elif !(DECODE_ABLATE & 4) && DECODE_CELL == 3
+        // two passes over 64-row stages (two 32-row gate tiles, two MFMA chains per wave):
+        //   pass 1: b_i + Wi.x for every tile -> lane scratch (h not live)
+        //   pass 2: partial + b_h + Wh.h, folded per 32-unit block U as the gates complete in
+        //           the order g1, g2, i, f, o (x not live): g = max(g1, g2); ig*g; c' = f*c + ig*g;
+        //           h' = o*tanh(c') -- the operations of nn_lstm_cell, in its order
+        {
+            PROF_STAMP(2);
+            auto tile_q = [](int m) { const int j = m % 5; return j < 2 ? j + 3 : j - 2; };   // 3,4,0,1,2
+            auto cell_load = [&](uint32_t w_off, uint32_t b_off, int j, Stage64Regs& r) {
+                const int ma = 2 * j, mb = 2 * j + 1;
+                const uint32_t ra = (uint32_t)(tile_q(ma) * 128 + 32 * (ma / 5));
+                const uint32_t rb = (uint32_t)(tile_q(mb) * 128 + 32 * (mb / 5));
+                const int l = lane_fresh();
+                const uint32_t vo = 16u * (uint32_t)(wave * 64 + l);
+                const uint32_t sa = 4u * (w_off + ra * 128u), sb = 4u * (w_off + rb * 128u);
+                // lane offsets stay non-negative (the buffer range check is on the lane offset)
+                const uint32_t rm = min(ra, rb);
+                const uint32_t vb = 4u * (uint32_t)(l & 31) + 4u * ((l & 32) ? rb - rm : ra - rm);
+                r.bw = ld1(theta_r, vb, 4u * (b_off + rm));
+                r.bz = ld1(noise_r, vb, 4u * (b_off + rm));
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t so = (u < 2 ? sa : sb) + 8192u * (uint32_t)(u & 1);
+                    r.w[u] = ld4s(theta_r, vo, so);
+                    r.z[u] = ld4s(noise_r, vo, so);
+                }
+            };
+            Stage64Regs cr;
+            // ---- pass 1
+            cell_load((uint32_t)p.off_i2h_w, (uint32_t)p.off_i2h_b, 0, cr);
+            stage64_store(lds, 0, 64, sigma, wave * 64 + lane_fresh(), cr);
+            __syncthreads();
+            for (int j = 0; j < 10; ++j) {
+                cell_load((uint32_t)p.off_i2h_w, (uint32_t)p.off_i2h_b, min(j + 1, 9), cr);
+                const float* buf = lds + (j & 1) * STAGE64_FLOATS;
+                f32x16 a0, a1;
+                mfma_stage64(buf + sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * sgn, xB, lane_fresh(), a0, a1);
+                const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
+                const int qa = tile_q(2 * j), qb = tile_q(2 * j + 1), ua = (2 * j) / 5, ub = (2 * j + 1) / 5;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) st1(scr_r, lo_, P_SLOT(16 * (5 * ua + qa) + r), a0[r]);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) st1(scr_r, lo_, P_SLOT(16 * (5 * ub + qb) + r), a1[r]);
+                stage64_store(lds + ((j + 1) & 1) * STAGE64_FLOATS, 0, 64, sigma, wave * 64 + lane_fresh(), cr);
+                __syncthreads();
+            }
+            PROF_STAMP(3);
+            // ---- pass 2
+#pragma unroll
+            for (int i = 0; i < 64; ++i) hB[i] = (t == 0) ? 0.f : ld1(scr_r, lo, H_SLOT(i));
+            cell_load((uint32_t)p.off_h2h_w, (uint32_t)p.off_h2h_b, 0, cr);
+            stage64_store(lds, 0, 64, sigma, wave * 64 + lane_fresh(), cr);
+            __syncthreads();
+            f32x16 hold;
+            auto fold = [&](int m, const f32x16& acc, uint32_t lo_) {
+                const int U = m / 5, j5 = m % 5;
+                if (j5 == 0) {                                   // g1
+                    hold = acc;
+                } else if (j5 == 1) {                            // g = max(g1, g2)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) hold[r] = hold[r] > acc[r] ? hold[r] : acc[r];
+                } else if (j5 == 2) {                            // ig * g
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) hold[r] = nn_sigmoidf(acc[r]) * hold[r];
+                } else if (j5 == 3) {                            // c' = f * c + ig * g
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float cold = (t == 0) ? 0.f : ld1(scr_r, lo_, C_SLOT(16 * U + r));
+                        const float fcv = nn_sigmoidf(acc[r]) * cold;
+                        const float cn = fcv + hold[r];
+                        st1(scr_r, lo_, C_SLOT(16 * U + r), cn);
+                        hold[r] = cn;
+                    }
+                } else {                                         // h' = o * tanh(c')
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        st1(scr_r, lo_, H_SLOT(16 * U + r), nn_sigmoidf(acc[r]) * nn_tanhf(hold[r]));
+                }
+            };
+            for (int j = 0; j < 10; ++j) {
+                const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
+                const int ma = 2 * j, mb = 2 * j + 1;
+                f32x16 a0, a1;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) a0[r] = ld1(scr_r, lo_, P_SLOT(16 * (5 * (ma / 5) + tile_q(ma)) + r));
+#pragma unroll
+                for (int r = 0; r < 16; ++r) a1[r] = ld1(scr_r, lo_, P_SLOT(16 * (5 * (mb / 5) + tile_q(mb)) + r));
+                __builtin_amdgcn_sched_barrier(0);
+                cell_load((uint32_t)p.off_h2h_w, (uint32_t)p.off_h2h_b, min(j + 1, 9), cr);
+                const float* buf = lds + (j & 1) * STAGE64_FLOATS;
+                const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * sgn;
+                const int hh_ = lane_fresh() >> 5;
+                a0 = a0 + bias_init(bsg, hh_);
+                a1 = a1 + bias_init(bsg + 32, hh_);
+                if (t > 0) mfma_stage64_acc(buf + sgn * (64 * LDS_ROW), hB, lane_fresh(), a0, a1);   // h = 0 at t = 0
+                fold(ma, a0, lo_);
+                fold(mb, a1, lo_);
+                stage64_store(lds + ((j + 1) & 1) * STAGE64_FLOATS, 0, 64, sigma, wave * 64 + lane_fresh(), cr);
+                __syncthreads();
+            }
+            PROF_STAMP(4);
+#pragma unroll
+            for (int i = 0; i < 64; ++i) hB[i] = ld1(scr_r, lo, H_SLOT(i));
+        }
 #elif !(DECODE_ABLATE & 4)
         {
             PROF_STAMP(2);
@@ -718,6 +1162,54 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
         PROF_STAMP(5);
         RowState st;
         row_state_init(st);
+#if DECODE_GLDS
+        glds_issue(lw_r, lz_r, lbw_r, lbz_r, lds, 0, wave);
+        glds_form(lds, 0, p.V1, sigma, wave);
+        __syncthreads();
+        f32x16 prev0, prev1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { prev0[r] = NEG_INF; prev1[r] = NEG_INF; }
+        for (int s = 0; s < nst; ++s) {
+            const bool more = s + 1 < nst;
+            float* nbuf = lds + ((s + 1) & 1) * GST_FLOATS;
+#if DECODE_PROF >= 2
+            PROF_STAMP(8);
+#endif
+            if (more) glds_issue(lw_r, lz_r, lbw_r, lbz_r, nbuf, s + 1, wave);
+#if DECODE_PROF >= 2
+            PROF_STAMP(9);
+#endif
+            const float* buf = lds + (s & 1) * GST_FLOATS;
+            const float* wsg = buf + sgn * (64 * 128);
+            const float* bsg = buf + 2 * 64 * 128 + 64 * sgn;
+            f32x16 acc0, acc1;
+            if (sgn == 0) {
+                mfma_stage64_g(wsg, bsg, hB, lane_fresh(), acc0, acc1);
+                epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
+            } else {
+                epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
+                mfma_stage64_g(wsg, bsg, hB, lane_fresh(), acc0, acc1);
+            }
+#if DECODE_PROF >= 2
+            PROF_STAMP(10);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            PROF_STAMP(12);
+#endif
+            if (more) glds_form(nbuf, s + 1, p.V1, sigma, wave);
+#if DECODE_PROF >= 2
+            PROF_STAMP(11);
+#endif
+            __syncthreads();
+#if DECODE_PROF >= 2
+            PROF_STAMP(5);
+#endif
+            prev0 = acc0;
+            prev1 = acc1;
+        }
+#else
+#ifdef LOGIT_PRIO_SGN
+        if (sgn == LOGIT_PRIO_SGN) __builtin_amdgcn_s_setprio(1);   // static priority for one half
+#endif
         Stage64Regs s64;
         stage64_load(lw_r, lz_r, lbw_r, lbz_r, 0, tid, s64);
         stage64_store(lds, 0, p.V1, sigma, tid, s64);
@@ -739,7 +1231,12 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
             const float* wsg = buf + sgn * (64 * LDS_ROW);
             const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * sgn;
             f32x16 acc0, acc1;
+#if DECODE_IEPI
+            mfma_stage64_iepi(wsg, bsg, hB, lane_fresh(), acc0, acc1, st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
+            if (false) {
+#else
             if (sgn == 0) {
+#endif
                 mfma_stage64(wsg, bsg, hB, lane_fresh(), acc0, acc1);
 #if !(DECODE_ABLATE & 1)
                 epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
@@ -768,7 +1265,11 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
             prev0 = acc0;
             prev1 = acc1;
         }
+#endif
         epilogue64(st, prev0, prev1, 64 * (nst - 1) + 4 * hh);
+#ifdef LOGIT_PRIO_SGN
+        __builtin_amdgcn_s_setprio(0);
+#endif
         PROF_STAMP(6);
         // merge the two lane halves that share this batch row
         const float m_o = __shfl_xor(st.m, 32);

@@ -44,6 +44,9 @@ struct nicnes_handle {
     const uint64_t* df_keys = nullptr;
     const double* df_vals = nullptr;
     int64_t df_n = 0;
+    uint64_t* hash_keys = nullptr;   // engine-owned open-addressing copy of the df table
+    double* hash_vals = nullptr;
+    uint64_t hash_mask = 0;
     double ref_len = 0.0;
     bool df_set = false;
 
@@ -201,7 +204,8 @@ int nicnes_destroy(nicnes_handle* h) {
     if (!h) return NICNES_OK;
     (void)hipSetDevice(h->device);
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
-                    h->ref_norm, h->nidx, h->seq, h->dscratch, h->stats, h->partials, h->norms};
+                    h->ref_norm, h->nidx, h->seq, h->dscratch, h->stats, h->partials, h->norms,
+                    h->hash_keys, h->hash_vals};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : h->ev)
@@ -270,6 +274,9 @@ static CiderTables tables_of(nicnes_handle* h) {
     tb.df_keys = h->df_keys;
     tb.df_vals = h->df_vals;
     tb.df_n = h->df_n;
+    tb.hash_keys = h->hash_keys;
+    tb.hash_vals = h->hash_vals;
+    tb.hash_mask = h->hash_mask;
     tb.ref_len = h->ref_len;
     tb.ref_keys = h->ref_keys;
     tb.ref_vec = h->ref_vec;
@@ -281,6 +288,20 @@ static CiderTables tables_of(nicnes_handle* h) {
 
 int nicnes_set_df_table(nicnes_handle* h, const uint64_t* keys, const double* df, int64_t n, double ref_len_log) {
     if (!h || n < 0 || (n > 0 && (!keys || !df))) return NICNES_ERR_INVALID;
+    HIPC(h, hipSetDevice(h->device));
+    if (h->hash_keys) (void)hipFree(h->hash_keys);
+    if (h->hash_vals) (void)hipFree(h->hash_vals);
+    h->hash_keys = nullptr;
+    h->hash_vals = nullptr;
+    const uint64_t cap = nicnes_df_hash_capacity(n);
+    int rc = dalloc(h, &h->hash_keys, cap);
+    if (rc) return rc;
+    rc = dalloc(h, &h->hash_vals, cap);
+    if (rc) return rc;
+    HIPC(h, hipMemset(h->hash_keys, 0, cap * sizeof(uint64_t)));
+    HIPC(h, nicnes_launch_df_hash_build(keys, df, n, h->hash_keys, h->hash_vals, cap - 1, nullptr));
+    HIPC(h, hipDeviceSynchronize());
+    h->hash_mask = cap - 1;
     h->df_keys = keys;
     h->df_vals = df;
     h->df_n = n;

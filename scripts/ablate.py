@@ -50,13 +50,13 @@ def main():
     for k in [x for x in engines if x.startswith('prof')]:   # DECODE_PROF builds: section cycles
         _, seq = engines[k].evaluate(50, 0, pop, 0.01, return_seq=True)
         cyc = seq.view(pop, -1)[:, :128].reshape(pop, 8, 16).double().cpu().numpy()   # [member, wave, section]
-        names = ['img', 'embed', 'cell_p1', 'cell_p2', 'cell_elem', 'logit', 'finish', 'tail', 'lg_top',
-                 'lg_load', 'lg_mfma_epi', 'lg_store', 's12', 's13', 's14', 's15']
+        names = ['img', 'embed', 'cell_p1', 'cell_p2', 'cell_elem', 'logit', 'finish', 'tail', 'lg_issue',
+                 'lg_mfma_epi', 'lg_store_or_wait', 'lg_barrier', 'lg_form', 's13', 's14', 's15']
         tot = cyc.sum(axis=2).mean()
         print(k, 'mean cycles per wave:', json.dumps({n: round(float(cyc[:, :, i].mean()), 0) for i, n in enumerate(names)}),
               'total', round(float(tot), 0), 'frac', json.dumps({n: round(float(cyc[:, :, i].mean() / tot), 4)
                                                                    for i, n in enumerate(names)}))
-        for i in (5, 8, 9, 10, 11):
+        for i in (5, 8, 9, 10, 11, 12):
             print(k, names[i], 'sgn0 %.0f sgn1 %.0f' % (cyc[:, :4, i].mean(), cyc[:, 4:, i].mean()))
     base = np.median(res['base'])
     out = {k: {'median_ms': round(float(np.median(v)), 3), 'min_ms': round(float(np.min(v)), 3),
