@@ -595,6 +595,23 @@ __device__ __forceinline__ void records16(RowState& st, const f32x16& P, int vba
     }
 }
 
+#ifndef DECODE_REC
+#define DECODE_REC 1       // 2: newest record + previous record's value only (index as a scalar key)
+#endif
+// REC 2: per element one compare and three selects. The index is kept as the wave-uniform key
+// kbase + (r&3) + 8(r>>2) (vocab index minus this lane half's 4*hh); the previous record keeps
+// only its value -- if it lands in the tie window the row takes the exact pass.
+__device__ __forceinline__ void records16_k(RowState& st, const f32x16& P, int kbase) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float L = P[r];
+        const bool c = L > st.r1v;
+        st.r0v = c ? st.r1v : st.r0v;
+        st.r1v = c ? L : st.r1v;
+        st.r1i = c ? kbase + (r & 3) + 8 * (r >> 2) : st.r1i;
+    }
+}
+
 // epilogue of one stage: P0 holds vocab vbase + (r&3) + 8(r>>2), P1 the same + 32.
 // Record scans run only in the (wave-uniform) case that some lane sees a new running max.
 __device__ __forceinline__ void epilogue64(RowState& st, const f32x16& P0, const f32x16& P1, int vbase) {
@@ -616,8 +633,14 @@ __device__ __forceinline__ void epilogue64(RowState& st, const f32x16& P0, const
     st.s = s;
     st.m = mnew;
     if (__any(tmax > st.r1v)) {
+#if DECODE_REC == 2
+        const int kbase = __builtin_amdgcn_readfirstlane(vbase) & ~7;    // vbase = 64 (s-1) + 4 hh
+        records16_k(st, P0, kbase);
+        records16_k(st, P1, kbase + 32);
+#else
         records16(st, P0, vbase);
         records16(st, P1, vbase + 32);
+#endif
     }
 }
 
@@ -1278,6 +1301,17 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
         const float stot = st.s * __builtin_amdgcn_exp2f((st.m - m) * LOG2E) + s_o * __builtin_amdgcn_exp2f((m_o - m) * LOG2E);
         const float lse = logf(stot);
         int tok = 0x7fffffff;
+#if DECODE_REC == 2
+        {
+            const int own = (int)((uint32_t)st.r1i + 4u * (uint32_t)hh);   // key -> vocab index of this lane half
+            const float cv[2] = {st.r1v, __shfl_xor(st.r1v, 32)};
+            const int ci[2] = {own, __shfl_xor(own, 32)};
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (in_window(cv[k], m, lse) && ci[k] < tok) tok = ci[k];
+        }
+        const bool ovf = in_window(st.r0v, m, lse) || in_window(__shfl_xor(st.r0v, 32), m, lse);
+#else
         {
             const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
             const int ci[4] = {st.r0i, st.r1i, __shfl_xor(st.r0i, 32), __shfl_xor(st.r1i, 32)};
@@ -1286,6 +1320,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
                 if (in_window(cv[k], m, lse) && ci[k] < tok) tok = ci[k];
         }
         const bool ovf = in_window(st.ev, m, lse) || in_window(__shfl_xor(st.ev, 32), m, lse);
+#endif
         if (__syncthreads_or(ovf ? 1 : 0)) {
             // rare: more records than tracked fall in the tie window -> exact second pass
             int best = 0x7fffffff;
