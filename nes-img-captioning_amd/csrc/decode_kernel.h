@@ -13,6 +13,7 @@ struct DecodeParams {
     float* scratch;              // nicnes_decode_scratch_floats(): lane-private c | h' | gate partials
     int32_t* stats;              // [0] = exact-pass fallbacks (atomic)
     float sigma;
+    int32_t force_exact;         // test hook (NICNES_FORCE_EXACT=1): every step takes the exact tie pass
     int32_t B, F, V1, T;
     int64_t D;
     int64_t off_img_w, off_img_b, off_emb_w, off_log_w, off_log_b, off_i2h_w, off_i2h_b, off_h2h_w, off_h2h_b;

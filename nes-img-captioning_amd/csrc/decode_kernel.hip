@@ -1310,7 +1310,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
             for (int k = 0; k < 2; ++k)
                 if (in_window(cv[k], m, lse) && ci[k] < tok) tok = ci[k];
         }
-        const bool ovf = in_window(st.r0v, m, lse) || in_window(__shfl_xor(st.r0v, 32), m, lse);
+        const bool ovf = p.force_exact || in_window(st.r0v, m, lse) || in_window(__shfl_xor(st.r0v, 32), m, lse);
 #else
         {
             const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
@@ -1319,7 +1319,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_kernel(DecodeParams p)
             for (int k = 0; k < 4; ++k)
                 if (in_window(cv[k], m, lse) && ci[k] < tok) tok = ci[k];
         }
-        const bool ovf = in_window(st.ev, m, lse) || in_window(__shfl_xor(st.ev, 32), m, lse);
+        const bool ovf = p.force_exact || in_window(st.ev, m, lse) || in_window(__shfl_xor(st.ev, 32), m, lse);
 #endif
         if (__syncthreads_or(ovf ? 1 : 0)) {
             // rare: more records than tracked fall in the tie window -> exact second pass

@@ -64,6 +64,7 @@ struct nicnes_handle {
     double* norms = nullptr;
 
     bool timing = false;
+    int force_exact = 0;      // test hook: exact tie pass on every step (NICNES_FORCE_EXACT=1)
     int decode_variant = 2;   // 2: two waves per SIMD (decode_kernel.hip, default); 1: one wave per
                               // SIMD, both signs per wave (decode_w1.hip, NICNES_DECODE=1)
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -176,6 +177,8 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
     {
         const char* v = getenv("NICNES_DECODE");
         if (v && v[0] == '1') h->decode_variant = 1;
+        const char* fe = getenv("NICNES_FORCE_EXACT");
+        h->force_exact = (fe && fe[0] == '1') ? 1 : 0;
     }
     if (!rc) {
         const size_t a = nicnes_decode_scratch_floats((int)MM, nslabs_of((int)MB));
@@ -358,6 +361,7 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
     p.scratch = h->dscratch;
     p.stats = h->stats;
     p.sigma = sigma;
+    p.force_exact = h->force_exact;
     p.B = h->B;
     p.F = h->cfg.fc_feat_size;
     p.V1 = h->V1;

@@ -272,3 +272,26 @@ def test_engine_worker_and_dispatched_master(eng):
         mc.declare_task = declare_and_work
         master.run_dispatched(mc, [batch], max_iterations=1, result_timeout=60)
     assert np.array_equal(eng.theta()[0].cpu().numpy(), want)
+
+
+def test_exact_tie_pass_matches_oracle(monkeypatch):
+    """The exact second pass of the greedy tie rule (normally taken only when more records than
+    tracked fall in the log_softmax tie window) forced on every step: tokens still match."""
+    import nicnes
+    monkeypatch.setenv('NICNES_FORCE_EXACT', '1')
+    e = nicnes.Engine(max_batch=64, max_members=2, noise_len=NOISE_LEN, noise_seed=7)
+    try:
+        table = O.noise_table(NOISE_LEN, 123)
+        e.set_noise_table(table)
+        dims = O.Dims()
+        theta = O.make_theta(dims, 5, 4.0, 0.1)
+        fc = np.random.Generator(np.random.PCG64(4321)).standard_normal((40, dims.F)).astype(np.float32)
+        _load(e, theta, fc)
+        _, seq = e.evaluate(3, 0, 1, SIGMA, return_seq=True)
+        seq = seq.cpu().numpy()
+        assert e.stats()['tie_fallbacks'] >= 16          # one per decode step of the workgroup
+        idx = int(e.noise_indices(3, 0, 1).cpu().numpy()[0])
+        for s, (oseq, fr) in enumerate(_oracle_member(theta, table, idx, fc, dims)):
+            assert _compare_tokens(seq[0, s], oseq, fr) == 0
+    finally:
+        e.close()

@@ -92,7 +92,7 @@ def test_tokens_match_oracle(eng, B, bu):
     _, seq = eng.evaluate(6, 1, 1, SIGMA, return_seq=True)
     seq = seq.cpu().numpy()[0]
     idx = int(eng.noise_indices(6, 1, 1).cpu().numpy()[0])
-    rows = [0, 31, 32, 127] + ([128, 129] if B > 128 else [B - 1])
+    rows = sorted({0, 31, 32, min(127, B - 1), B - 1} | ({128, 129} if B > 128 else set()))
     for s, sign in enumerate((+1, -1)):
         oseq, _, fr = O.decode(dims, O.perturb(theta, eng._table_np, idx, SIGMA, sign), fc[rows])
         for j, b in enumerate(rows):
@@ -111,8 +111,8 @@ def _tie_theta(dims, base_theta, fc, copies):
     th = base_theta.copy()
     o = dims.offsets()
     V1, R = dims.vocab_size + 1, dims.R
-    lw = th[o[3]:o[3] + V1 * R].reshape(V1, R)
-    lb = th[o[4]:o[4] + V1]
+    lw = th[o['logit.weight'][0]:o['logit.weight'][0] + V1 * R].reshape(V1, R)
+    lb = th[o['logit.bias'][0]:o['logit.bias'][0] + V1]
     for where, k in copies:
         dst = {'lower': max(tok // 2, 1), 'higher': min(tok + 8, V1 - 1), 'higher2': min(tok + 16, V1 - 1)}[where]
         lw[dst] = lw[tok]
