@@ -17,12 +17,24 @@ struct CiderTables {
     int32_t* ref_count;        // [n_refs]
     int32_t* ref_len2;         // [n_refs] bigram count
     double* ref_norm;          // [n_refs, 4]
+    // per-image n-gram tables (written by nicnes_img_ngram_kernel): the union of the image's
+    // reference n-grams, hashed to a row of per-reference tf-idf weights
+    uint64_t* img_hkey;        // [B, IMG_CAP] (0 = empty)
+    int32_t* img_hrow;         // [B, IMG_CAP]
+    double* img_vr;            // [B, IMG_ROWS, IMG_MAXR]
 };
+#define IMG_CAP 1024
+#define IMG_ROWS 512
+#define IMG_MAXR 8
 
 extern "C" uint64_t nicnes_df_hash_capacity(int64_t n);
 extern "C" hipError_t nicnes_launch_df_hash_build(const uint64_t* keys, const double* vals, int64_t n, uint64_t* hkeys,
                                                   double* hvals, uint64_t mask, hipStream_t stream);
 extern "C" hipError_t nicnes_launch_cook_refs(const int32_t* ref_tokens, int n_refs, int T, const CiderTables* tb,
                                               hipStream_t stream);
+extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int B, const CiderTables* tb,
+                                               hipStream_t stream);
+extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
+                                              const int32_t* img_ref_start, double* fitness_out, hipStream_t stream);
 extern "C" hipError_t nicnes_launch_cider(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
                                           const int32_t* img_ref_start, double* fitness_out, hipStream_t stream);

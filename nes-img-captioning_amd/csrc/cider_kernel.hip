@@ -221,3 +221,111 @@ extern "C" hipError_t nicnes_launch_cider(const int32_t* seq, int n_cand, int B,
     hipLaunchKernelGGL(nicnes_cider_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, *tb, img_ref_start, fitness_out);
     return hipGetLastError();
 }
+
+// ---- per-image reference n-gram tables (one wave per image, built once per batch) ------------
+__global__ __launch_bounds__(64) void nicnes_img_ngram_kernel(const int32_t* img_ref_start, CiderTables tb) {
+    __shared__ unsigned long long hk[IMG_CAP];
+    __shared__ int hr[IMG_CAP];
+    __shared__ int nrows;
+    const int lane = threadIdx.x, b = blockIdx.x;
+    for (int i = lane; i < IMG_CAP; i += 64) { hk[i] = 0ull; hr[i] = -1; }
+    if (lane == 0) nrows = 0;
+    __syncthreads();
+    const int r0 = img_ref_start[b], r1 = img_ref_start[b + 1];
+    for (int r = r0; r < r1 && r - r0 < IMG_MAXR; ++r) {
+        const int cnt = tb.ref_count[r];
+        if (lane < cnt) {
+            const unsigned long long key = tb.ref_keys[(size_t)r * REF_SLOTS + lane];
+            uint32_t slot = (uint32_t)df_hash(key) & (IMG_CAP - 1);
+            int row = -1;
+            for (int probe = 0; probe < IMG_CAP; ++probe) {
+                const unsigned long long prev = atomicCAS(&hk[slot], 0ull, key);
+                if (prev == 0ull) {                      // new n-gram of this image
+                    row = atomicAdd(&nrows, 1);
+                    hr[slot] = row;
+                    break;
+                }
+                if (prev == key) {                       // seen in an earlier reference
+                    row = hr[slot];
+                    break;
+                }
+                slot = (slot + 1) & (IMG_CAP - 1);
+            }
+            if (row >= 0 && row < IMG_ROWS)
+                tb.img_vr[((size_t)b * IMG_ROWS + row) * IMG_MAXR + (r - r0)] = tb.ref_vec[(size_t)r * REF_SLOTS + lane];
+        }
+        __syncthreads();
+    }
+    for (int i = lane; i < IMG_CAP; i += 64) {
+        tb.img_hkey[(size_t)b * IMG_CAP + i] = hk[i];
+        tb.img_hrow[(size_t)b * IMG_CAP + i] = hr[i];
+    }
+}
+
+// candidates scored against the image table: one probe per distinct n-gram, then the per-reference
+// weights are consecutive doubles (same arithmetic and order as nicnes_cider_kernel)
+__global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* seq, int B, int T, CiderTables tb,
+                                                               const int32_t* img_ref_start, double* fitness_out) {
+    __shared__ double row_score[1024];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int cand = blockIdx.x;
+    const double sigma2x2 = 2.0 * 6.0 * 6.0;
+    for (int b = wave; b < B; b += 4) {
+        const int32_t* row = seq + ((size_t)cand * B + b) * T;
+        const NgramLane g = ngram_lane(row, T, lane, tb);
+        const double nh = sqrt(seg_sum(g.first ? g.vec * g.vec : 0.0));
+        const int L = caption_len(row, T);
+        const int len_h = L > 1 ? L - 1 : 0;
+        int trow = -1;
+        if (g.first) {
+            uint32_t slot = (uint32_t)df_hash(g.key) & (IMG_CAP - 1);
+            for (int probe = 0; probe < IMG_CAP; ++probe) {
+                const uint64_t k = tb.img_hkey[(size_t)b * IMG_CAP + slot];
+                if (k == g.key) { trow = tb.img_hrow[(size_t)b * IMG_CAP + slot]; break; }
+                if (k == 0ull) break;
+                slot = (slot + 1) & (IMG_CAP - 1);
+            }
+        }
+        const double* vrow = tb.img_vr + ((size_t)b * IMG_ROWS + (trow >= 0 ? trow : 0)) * IMG_MAXR;
+        double score = 0.0;
+        const int r0 = img_ref_start[b], r1 = img_ref_start[b + 1];
+        for (int r = r0; r < r1; ++r) {
+            const double vr = trow >= 0 ? vrow[r - r0] : 0.0;
+            const double contrib = g.first ? (g.vec < vr ? g.vec : vr) * vr : 0.0;
+            const double delta = (double)(len_h - tb.ref_len2[r]);
+            const double pen = exp(-(delta * delta) / sigma2x2);
+            double val = seg_sum(contrib);
+            const double nr = tb.ref_norm[(size_t)r * 4 + (lane >> 4)];
+            if (nh != 0.0 && nr != 0.0) val /= (nh * nr);
+            score += val * pen;
+        }
+        score += __shfl_xor(score, 16);
+        score += __shfl_xor(score, 32);
+        if (lane == 0) {
+            double avg = score / 4.0;
+            avg /= (double)(r1 - r0);
+            avg *= 10.0;
+            row_score[b] = avg;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int b = 0; b < B; ++b) s += row_score[b];
+        fitness_out[cand] = (s / (double)B) * 100.0;        // float(cider * 100), policies.py:125
+    }
+}
+
+extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int B, const CiderTables* tb,
+                                               hipStream_t stream) {
+    hipLaunchKernelGGL(nicnes_img_ngram_kernel, dim3(B), dim3(64), 0, stream, img_ref_start, *tb);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
+                                              const int32_t* img_ref_start, double* fitness_out, hipStream_t stream) {
+    if (B > 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(nicnes_cider_img_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, *tb, img_ref_start,
+                       fitness_out);
+    return hipGetLastError();
+}

@@ -10,6 +10,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
+#include <algorithm>
 
 #include "../../include/nicnes.h"
 #include "cider_kernel.h"
@@ -50,6 +52,10 @@ struct nicnes_handle {
     double ref_len = 0.0;
     bool df_set = false;
 
+    uint64_t* img_hkey = nullptr;     // per-image reference n-gram tables (CIDEr-D)
+    int32_t* img_hrow = nullptr;
+    double* img_vr = nullptr;
+    bool img_tables = false;          // every image has <= IMG_MAXR references
     uint64_t* ref_keys = nullptr;
     double* ref_vec = nullptr;
     int32_t* ref_count = nullptr;
@@ -172,6 +178,9 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
     if (!rc) rc = dalloc(h, &h->ref_count, MR);
     if (!rc) rc = dalloc(h, &h->ref_len2, MR);
     if (!rc) rc = dalloc(h, &h->ref_norm, MR * 4);
+    if (!rc) rc = dalloc(h, &h->img_hkey, MB * IMG_CAP);
+    if (!rc) rc = dalloc(h, &h->img_hrow, MB * IMG_CAP);
+    if (!rc) rc = dalloc(h, &h->img_vr, MB * IMG_ROWS * IMG_MAXR);
     if (!rc) rc = dalloc(h, &h->nidx, MM);
     if (!rc) rc = dalloc(h, &h->seq, MM * 2 * MB * T);
     {
@@ -208,7 +217,7 @@ int nicnes_destroy(nicnes_handle* h) {
     (void)hipSetDevice(h->device);
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
                     h->ref_norm, h->nidx, h->seq, h->dscratch, h->stats, h->partials, h->norms,
-                    h->hash_keys, h->hash_vals};
+                    h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : h->ev)
@@ -286,6 +295,9 @@ static CiderTables tables_of(nicnes_handle* h) {
     tb.ref_count = h->ref_count;
     tb.ref_len2 = h->ref_len2;
     tb.ref_norm = h->ref_norm;
+    tb.img_hkey = h->img_hkey;
+    tb.img_hrow = h->img_hrow;
+    tb.img_vr = h->img_vr;
     return tb;
 }
 
@@ -328,6 +340,21 @@ int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t
     h->img_ref_start = img_ref_start;
     CiderTables tb = tables_of(h);
     HIPC(h, nicnes_launch_cook_refs(ref_tokens, n_refs, h->cfg.seq_length, &tb, (hipStream_t)stream));
+    // per-image n-gram tables when every image has at most IMG_MAXR references (else the
+    // per-reference scan kernel scores the candidates)
+    {
+        std::vector<int32_t> st((size_t)B + 1);
+        HIPC(h, hipMemcpyAsync(st.data(), img_ref_start, st.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
+                               (hipStream_t)stream));
+        HIPC(h, hipStreamSynchronize((hipStream_t)stream));
+        int maxr = 0;
+        for (int b = 0; b < B; ++b) maxr = std::max(maxr, st[b + 1] - st[b]);
+        h->img_tables = maxr <= IMG_MAXR;
+    }
+    if (h->img_tables) {
+        HIPC(h, hipMemsetAsync(h->img_vr, 0, (size_t)B * IMG_ROWS * IMG_MAXR * sizeof(double), (hipStream_t)stream));
+        HIPC(h, nicnes_launch_img_ngrams(img_ref_start, B, &tb, (hipStream_t)stream));
+    }
     h->batch_set = true;
     return NICNES_OK;
 }
@@ -383,7 +410,10 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
     else HIPC(h, nicnes_launch_decode_w1(&p, count, nslabs_of(h->B), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     CiderTables tb = tables_of(h);
-    HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, fitness_out, s));
+    if (h->img_tables)
+        HIPC(h, nicnes_launch_cider_img(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, fitness_out, s));
+    else
+        HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, fitness_out, s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[2], s));
     return NICNES_OK;
 }

@@ -90,7 +90,9 @@ def test_decode_tiny_batch_and_slabs(eng):
         assert _compare_tokens(seq5.cpu().numpy()[0, s], oseq, fr) == 0
 
 
-def test_cider_fitness_matches_oracle(eng):
+@pytest.mark.parametrize('n_refs', [5, 10], ids=['image_tables', 'scan_over_8_refs'])
+def test_cider_fitness_matches_oracle(eng, n_refs):
+    """5 refs per image: the per-image n-gram table kernel; 10 (> IMG_MAXR): the per-reference scan."""
     import nicnes.synthetic as S
     dims = O.Dims()
     theta = O.make_theta(dims, 0, 4.0, 0.1)
@@ -98,7 +100,7 @@ def test_cider_fitness_matches_oracle(eng):
     fc = np.random.Generator(np.random.PCG64(1234)).standard_normal((B, dims.F)).astype(np.float32)
     # references derived from the oracle's own base caption
     base, _, _ = O.decode(dims, theta, fc)
-    gts, df, ref_len_raw = S.build_references(base, dims.vocab_size, seed=11, df_sets=256)
+    gts, df, ref_len_raw = S.build_references(base, dims.vocab_size, seed=11, n_refs=n_refs, df_sets=256)
     _load(eng, theta, fc, gts, df, ref_len_raw)
     fit, seq = eng.evaluate(2, 0, 3, SIGMA, return_seq=True)
     fit, seq = fit.cpu().numpy(), seq.cpu().numpy()
