@@ -1,6 +1,6 @@
 // Internal (non-ABI) launch interfaces of the engine's kernels.
 #pragma once
-#define SCR_SLOTS (64 + 64 + 320)   // per lane: c | h' | 20 partial gate tiles
+#define SCR_SLOTS (64 + 64 + 320 + 64 + 2)   // per lane: c | h' | 20 h2h gate tiles | x of t = 0 | unfinished | token
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -12,6 +12,7 @@ struct DecodeParams {
     int32_t* seq;                // out: [members, 2, B, T] greedy tokens (masked after the first 0)
     float* scratch;              // nicnes_decode_scratch_floats(): lane-private c | h' | gate partials
     int32_t* stats;              // [0] = exact-pass fallbacks (atomic)
+    int32_t* alive;              // [members * slabs]: 0 once every row of the workgroup finished
     float sigma;
     int32_t force_exact;         // test hook (NICNES_FORCE_EXACT=1): every step takes the exact tie pass
     int32_t B, F, V1, T;
@@ -21,5 +22,3 @@ struct DecodeParams {
 
 extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream);
 extern "C" size_t nicnes_decode_scratch_floats(int member_count, int nslabs);
-extern "C" hipError_t nicnes_launch_decode_w1(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream);
-extern "C" size_t nicnes_decode_w1_scratch_floats(int member_count, int nslabs);

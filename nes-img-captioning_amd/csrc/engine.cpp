@@ -66,13 +66,12 @@ struct nicnes_handle {
     int32_t* seq = nullptr;
     float* dscratch = nullptr;
     int32_t* stats = nullptr;
+    int32_t* alive = nullptr;         // per decode workgroup: rows left unfinished
     double* partials = nullptr;
     double* norms = nullptr;
 
     bool timing = false;
     int force_exact = 0;      // test hook: exact tie pass on every step (NICNES_FORCE_EXACT=1)
-    int decode_variant = 2;   // 2: two waves per SIMD (decode_kernel.hip, default); 1: one wave per
-                              // SIMD, both signs per wave (decode_w1.hip, NICNES_DECODE=1)
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
 };
 
@@ -184,17 +183,12 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
     if (!rc) rc = dalloc(h, &h->nidx, MM);
     if (!rc) rc = dalloc(h, &h->seq, MM * 2 * MB * T);
     {
-        const char* v = getenv("NICNES_DECODE");
-        if (v && v[0] == '1') h->decode_variant = 1;
         const char* fe = getenv("NICNES_FORCE_EXACT");
         h->force_exact = (fe && fe[0] == '1') ? 1 : 0;
     }
-    if (!rc) {
-        const size_t a = nicnes_decode_scratch_floats((int)MM, nslabs_of((int)MB));
-        const size_t b = nicnes_decode_w1_scratch_floats((int)MM, nslabs_of((int)MB));
-        rc = dalloc(h, &h->dscratch, a > b ? a : b);
-    }
+    if (!rc) rc = dalloc(h, &h->dscratch, nicnes_decode_scratch_floats((int)MM, nslabs_of((int)MB)));
     if (!rc) rc = dalloc(h, &h->stats, 4);
+    if (!rc) rc = dalloc(h, &h->alive, MM * (size_t)nslabs_of((int)MB));
     if (!rc) rc = dalloc(h, &h->partials, 2 * (size_t)nicnes_adam_blocks(h->D));
     if (!rc) rc = dalloc(h, &h->norms, 2);
     if (rc) {
@@ -217,7 +211,7 @@ int nicnes_destroy(nicnes_handle* h) {
     (void)hipSetDevice(h->device);
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
                     h->ref_norm, h->nidx, h->seq, h->dscratch, h->stats, h->partials, h->norms,
-                    h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr};
+                    h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : h->ev)
@@ -387,6 +381,7 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
     p.seq = seq_out ? seq_out : h->seq;
     p.scratch = h->dscratch;
     p.stats = h->stats;
+    p.alive = h->alive;
     p.sigma = sigma;
     p.force_exact = h->force_exact;
     p.B = h->B;
@@ -406,8 +401,7 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
     // rows a member never writes (all finished early) must read as 0 (nets.py:188 zeros)
     HIPC(h, hipMemsetAsync(p.seq, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(int32_t), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
-    if (h->decode_variant == 2) HIPC(h, nicnes_launch_decode(&p, count, nslabs_of(h->B), s));
-    else HIPC(h, nicnes_launch_decode_w1(&p, count, nslabs_of(h->B), s));
+    HIPC(h, nicnes_launch_decode(&p, count, nslabs_of(h->B), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     CiderTables tb = tables_of(h);
     if (h->img_tables)

@@ -162,11 +162,12 @@ int od_decode(const od_dims* d, const float* theta, const float* fc, int B,
         for (int t = 0; t <= T; ++t) {
             if (t == 0) gemv_chain(WimgT, theta + L.img_b, fc + (size_t)b * F, E, F, half_order, x);
             else memcpy(x, theta + L.emb_w + (size_t)it * E, sizeof(float) * (size_t)E);
-            /* gate sums: one chain per gate, ((b_i2h + Wi.x) + b_h2h) + Wh.h (i2h then h2h, the
-             * order LSTMCore adds them, nets.py:109-111); h = 0 at t = 0 contributes nothing */
+            /* gate sums as LSTMCore forms them, all_input_sums = i2h(xt) + h2h(prev_h)
+             * (nets.py:109-111): two chains, (b_i2h + Wi.x) and (b_h2h + Wh.h), then one add.
+             * At t = 0, h = 0 and the h2h chain runs over zeros. */
             gemv_chain(WiT, theta + L.i2h_b, x, G, E, half_order, si);
-            for (int u = 0; u < G; ++u) sh[u] = si[u] + theta[L.h2h_b + u];
-            if (t > 0) gemv_chain_acc(WhT, h, G, R, half_order, sh);
+            gemv_chain(WhT, theta + L.h2h_b, h, G, R, half_order, sh);
+            for (int u = 0; u < G; ++u) sh[u] = si[u] + sh[u];
             for (int u = 0; u < R; ++u) {
                 float cn, hn;
                 nn_lstm_cell(sh[u], sh[R + u], sh[2 * R + u], sh[3 * R + u], sh[4 * R + u], c[u], &cn, &hn);
