@@ -128,6 +128,11 @@ int nicnes_stats(nicnes_handle* h, int64_t* out4_host);
 int nicnes_set_timing(nicnes_handle* h, int on);
 int nicnes_kernel_times(nicnes_handle* h, float* out2_host);
 
+/* Per-kernel split of the last timed decode (events between its launches): [0] = img-embed kernel
+ * ms, [1] = the T+1 LSTM-cell launches summed, [2] = the T+2 logit/h2h stage launches summed,
+ * [3] = the number of stage launches. Synchronising. */
+int nicnes_decode_phase_times(nicnes_handle* h, float* out4_host);
+
 #ifdef __cplusplus
 }
 #endif

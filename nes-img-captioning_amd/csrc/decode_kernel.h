@@ -20,5 +20,8 @@ struct DecodeParams {
     int64_t off_img_w, off_img_b, off_emb_w, off_log_w, off_log_b, off_i2h_w, off_i2h_b, off_h2h_w, off_h2h_b;
 };
 
-extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream);
+// evs (nullable): 2T + 5 events, recorded before the first launch and after every launch
+#define DECODE_MAX_EVENTS 64
+extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,
+                                           hipEvent_t* evs);
 extern "C" size_t nicnes_decode_scratch_floats(int member_count, int nslabs);

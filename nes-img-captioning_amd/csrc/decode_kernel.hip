@@ -689,7 +689,8 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_stage_kernel(DecodePar
     }
 }
 
-extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream) {
+extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,
+                                           hipEvent_t* evs) {
     const size_t lds64 = (size_t)(2 * STAGE64_FLOATS) * sizeof(float);
     const size_t lds32 = (size_t)(2 * STAGE_FLOATS) * sizeof(float);
     static bool attr_set = false;
@@ -699,12 +700,20 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
         if (e != hipSuccess) return e;
         attr_set = true;
     }
+    if (evs && 2 * p->T + 5 > DECODE_MAX_EVENTS) return hipErrorInvalidValue;
+    int ne = 0;
+    auto mark = [&]() { if (evs) (void)hipEventRecord(evs[ne++], stream); };
     const dim3 grid(member_count, nslabs), block(NTHREADS);
+    mark();
     hipLaunchKernelGGL(nicnes_decode_img_kernel, grid, block, lds32, stream, *p);
+    mark();
     hipLaunchKernelGGL(nicnes_decode_stage_kernel, grid, block, lds64, stream, *p, -1);
+    mark();
     for (int t = 0; t <= p->T; ++t) {
         hipLaunchKernelGGL(nicnes_decode_cell_kernel, grid, block, lds64, stream, *p, t);
+        mark();
         hipLaunchKernelGGL(nicnes_decode_stage_kernel, grid, block, lds64, stream, *p, t);
+        mark();
     }
     return hipGetLastError();
 }

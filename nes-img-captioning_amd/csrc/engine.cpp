@@ -73,6 +73,8 @@ struct nicnes_handle {
     bool timing = false;
     int force_exact = 0;      // test hook: exact tie pass on every step (NICNES_FORCE_EXACT=1)
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t dev[DECODE_MAX_EVENTS] = {};   // between the decode's launches (phase split)
+    int n_dev = 0;                            // events recorded by the last timed decode
 };
 
 namespace {
@@ -215,6 +217,8 @@ int nicnes_destroy(nicnes_handle* h) {
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : h->dev)
         if (e) (void)hipEventDestroy(e);
     delete h;
     return NICNES_OK;
@@ -401,7 +405,8 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
     // rows a member never writes (all finished early) must read as 0 (nets.py:188 zeros)
     HIPC(h, hipMemsetAsync(p.seq, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(int32_t), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
-    HIPC(h, nicnes_launch_decode(&p, count, nslabs_of(h->B), s));
+    HIPC(h, nicnes_launch_decode(&p, count, nslabs_of(h->B), s, h->timing ? h->dev : nullptr));
+    h->n_dev = h->timing ? 2 * p.T + 5 : 0;
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     CiderTables tb = tables_of(h);
     if (h->img_tables)
@@ -509,7 +514,10 @@ int nicnes_set_timing(nicnes_handle* h, int on) {
     if (!h) return NICNES_ERR_INVALID;
     HIPC(h, hipSetDevice(h->device));
     if (on && !h->ev[0])
+    {
         for (auto& e : h->ev) HIPC(h, hipEventCreate(&e));
+        for (auto& e : h->dev) HIPC(h, hipEventCreate(&e));
+    }
     h->timing = on != 0;
     return NICNES_OK;
 }
@@ -520,6 +528,25 @@ int nicnes_kernel_times(nicnes_handle* h, float* out2_host) {
     HIPC(h, hipEventSynchronize(h->ev[2]));
     HIPC(h, hipEventElapsedTime(&out2_host[0], h->ev[0], h->ev[1]));
     HIPC(h, hipEventElapsedTime(&out2_host[1], h->ev[1], h->ev[2]));
+    return NICNES_OK;
+}
+
+int nicnes_decode_phase_times(nicnes_handle* h, float* out4_host) {
+    if (!h || !out4_host || h->n_dev < 5) return NICNES_ERR_INVALID;
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, hipEventSynchronize(h->dev[h->n_dev - 1]));
+    // event k follows launch k: img, stage(-1), then cell(t), stage(t) for t = 0..T
+    float img = 0.f, cell = 0.f, stage = 0.f, ms = 0.f;
+    for (int k = 1; k < h->n_dev; ++k) {
+        HIPC(h, hipEventElapsedTime(&ms, h->dev[k - 1], h->dev[k]));
+        if (k == 1) img += ms;
+        else if (k % 2 == 0) stage += ms;
+        else cell += ms;
+    }
+    out4_host[0] = img;
+    out4_host[1] = cell;
+    out4_host[2] = stage;
+    out4_host[3] = (float)(h->n_dev / 2);
     return NICNES_OK;
 }
 

@@ -14,7 +14,8 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_set_noise_table', 'nicnes_set_theta', 'nicnes_get_theta', 'nicnes_set_adam_state',
            'nicnes_get_adam_state', 'nicnes_set_batch', 'nicnes_set_df_table', 'nicnes_noise_indices',
            'nicnes_evaluate', 'nicnes_rank_weights', 'nicnes_grad_partial', 'nicnes_adam_step', 'nicnes_stats',
-           'nicnes_set_timing', 'nicnes_kernel_times', 'nicnes_sgd_step', 'nicnes_optimizer_update']
+           'nicnes_set_timing', 'nicnes_kernel_times', 'nicnes_decode_phase_times', 'nicnes_sgd_step',
+           'nicnes_optimizer_update']
 
 
 class NicnesConfig(ctypes.Structure):
@@ -64,6 +65,7 @@ def lib(path=None):
         'nicnes_stats': (c.c_int, [vp, vp]),
         'nicnes_set_timing': (c.c_int, [vp, c.c_int]),
         'nicnes_kernel_times': (c.c_int, [vp, vp]),
+        'nicnes_decode_phase_times': (c.c_int, [vp, vp]),
         'nicnes_sgd_step': (c.c_int, [vp, vp, i32, f64, f64, f64, vp, vp]),
         'nicnes_optimizer_update': (c.c_int, [vp, c.c_int, vp, c.c_int, f64, f64, f64, f64, vp, vp]),
     }

@@ -218,6 +218,14 @@ class Engine:
         check(self.L.nicnes_kernel_times(self.h, out), self.h, 'kernel_times')
         return float(out[0]), float(out[1])
 
+    def decode_phase_times(self):
+        """Per-kernel split of the last timed decode: {'img_ms', 'cell_ms', 'stage_ms', 'stage_launches'}
+        (cell/stage summed over their T+1 / T+2 launches; HIP events between the launches)."""
+        out = (ctypes.c_float * 4)()
+        check(self.L.nicnes_decode_phase_times(self.h, out), self.h, 'decode_phase_times')
+        return {'img_ms': float(out[0]), 'cell_ms': float(out[1]), 'stage_ms': float(out[2]),
+                'stage_launches': int(out[3])}
+
     def stats(self):
         out = (ctypes.c_int64 * 4)()
         check(self.L.nicnes_stats(self.h, out), self.h, 'stats')

@@ -3,11 +3,12 @@
 Per /opt/skills/guides/MI355X_MICROARCH.md (HBM section): the counters are in KiB; on gfx950
 FETCH_SIZE reports half the bytes of a wide (16 B/lane) coalesced read, so
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
-Counter values are taken per dispatch of the kernel (all dispatches whose name matches, minus
-the first `--skip` ones, e.g. setup launches) and averaged.
+Counter values are taken per dispatch of the kernel (dispatches whose name matches and whose grid
+is the largest seen for it -- the bench's sigma = 0 single-member setup evaluate is dropped --
+minus the first `--skip` ones) and averaged.
 
-usage: python scripts/pmc_traffic.py --fetch DIR --write DIR --kernel nicnes_decode_kernel \
-           --skip 1 --algorithmic-bytes N --out profiles/r01_decode_pmc.json
+usage: python scripts/pmc_traffic.py --fetch DIR --write DIR --kernel nicnes_decode_stage_kernel \
+           --algorithmic-bytes N --out profiles/r01_decode_pmc.json
 """
 import argparse
 import csv
@@ -27,15 +28,20 @@ def per_dispatch(root, counter, kernel):
                 if row.get('Counter_Name') != counter or kernel not in row.get('Kernel_Name', ''):
                     continue
                 key = (fn, int(row['Dispatch_Id']))
-                vals[key] = vals.get(key, 0.0) + float(row['Counter_Value'])
-    return [vals[k] for k in sorted(vals)]
+                grid = int(row.get('Grid_Size', 0) or 0)
+                g, v = vals.get(key, (grid, 0.0))
+                vals[key] = (g, v + float(row['Counter_Value']))
+    if not vals:
+        return []
+    gmax = max(g for g, _ in vals.values())
+    return [vals[k][1] for k in sorted(vals) if vals[k][0] == gmax]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--fetch', required=True)
     ap.add_argument('--write', required=True)
-    ap.add_argument('--kernel', default='nicnes_decode_kernel')
+    ap.add_argument('--kernel', default='nicnes_decode_stage_kernel')
     ap.add_argument('--skip', type=int, default=0)
     ap.add_argument('--algorithmic-bytes', type=float, default=None)
     ap.add_argument('--out', required=True)
