@@ -104,10 +104,15 @@ int nicnes_grad_partial(nicnes_handle* h, uint64_t iteration, int32_t member_beg
                         float sigma, float* gsum_out, void* stream);
 
 /* g = gsum / (2P); globalg = -g + l2coeff * theta; Adam step on the engine's theta
- * (nic_nes_master.py:126-137, optimizers.py:15-22,78-83). Synchronising: returns the
- * update ratio |step| / |theta_old| in *ratio_out_host. */
+ * (nic_nes_master.py:126-137, optimizers.py:15-22,78-83). With ratio_out_host set it is
+ * synchronising and returns the update ratio |step| / |theta_old| there; with NULL it only
+ * enqueues, and nicnes_last_ratio reads the ratio later (so an iteration loop need not idle
+ * the GPU once per step). */
 int nicnes_adam_step(nicnes_handle* h, const float* gsum, int32_t P, double l2coeff, double stepsize, double beta1,
                      double beta2, double epsilon, double* ratio_out_host, void* stream);
+
+/* The update ratio of the newest optimizer step (synchronising on `stream`). */
+int nicnes_last_ratio(nicnes_handle* h, double* ratio_out_host, void* stream);
 
 /* SGD with momentum in the same fused form (src/algorithm/nic_nes/optimizers.py:38-47). */
 int nicnes_sgd_step(nicnes_handle* h, const float* gsum, int32_t P, double l2coeff, double stepsize, double momentum,

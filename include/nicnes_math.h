@@ -43,16 +43,17 @@ NN_FN float nn_pow2i(int32_t n) { return nn_i2f((n + 127) << 23); }
  * nn_expf: e^x, <= ~1 ulp. Cody-Waite reduction x = n ln2 + r, |r| <= ln2/2,
  * degree-7 Taylor in Horner form with fmaf, then scale by 2^n in two steps so
  * results in the subnormal range are formed exactly like on the host.
+ * Branch-free: the core runs on x clamped to [-104, 89] and the out-of-range / NaN results are
+ * selected at the end (one instruction stream for every lane of a wavefront); the values are
+ * those of the branchy form (tests/test_oracle_golden.py checks both against each other).
  */
 NN_FN float nn_expf(float x) {
-    if (x != x) return x;
-    if (x > 88.72283935546875f) return nn_i2f(0x7f800000);
-    if (x < -103.972084045410156f) return 0.0f;
     const float log2e = 1.44269502162933349609375f;
     const float ln2_hi = 0.693145751953125f;          /* 12 significant bits: n*ln2_hi exact */
     const float ln2_lo = 1.428606765330187045e-06f;
-    float n = nn_floorf(x * log2e + 0.5f);
-    float r = fmaf(-n, ln2_hi, x);
+    const float xc = fminf(fmaxf(x, -104.0f), 89.0f); /* NaN -> -104 (replaced below) */
+    float n = nn_floorf(xc * log2e + 0.5f);
+    float r = fmaf(-n, ln2_hi, xc);
     r = fmaf(-n, ln2_lo, r);
     float p = 1.98412701138295233250e-4f;             /* 1/7! */
     p = fmaf(p, r, 1.38888892251998186111e-3f);       /* 1/6! */
@@ -62,10 +63,12 @@ NN_FN float nn_expf(float x) {
     p = fmaf(p, r, 0.5f);
     p = fmaf(p, r, 1.0f);
     p = fmaf(p, r, 1.0f);
-    int32_t ni = (int32_t)n;
-    if (ni > 127) return p * nn_pow2i(127) * nn_pow2i(ni - 127);
-    if (ni < -126) return p * nn_pow2i(-126) * nn_pow2i(ni + 126);
-    return p * nn_pow2i(ni);
+    const int32_t ni = (int32_t)n;                    /* in [-150, 129] */
+    const int32_t n1 = ni > 127 ? 127 : (ni < -126 ? -126 : ni);
+    float y = p * nn_pow2i(n1) * nn_pow2i(ni - n1);   /* second factor 2^0 unless out of range */
+    y = x > 88.72283935546875f ? nn_i2f(0x7f800000) : y;
+    y = x < -103.972084045410156f ? 0.0f : y;
+    return x != x ? x : y;
 }
 
 /* sigmoid as torch.sigmoid defines it (src/captioning/nets.py:117): 1 / (1 + e^-x) */
@@ -73,25 +76,24 @@ NN_FN float nn_sigmoidf(float x) { return 1.0f / (1.0f + nn_expf(-x)); }
 
 /*
  * nn_tanhf: odd; |x| < 0.6 -> x * P(x^2) (least-squares fit of tanh(x)/x in double,
- * abs err 3.6e-10 before fp32 rounding), else 1 - 2/(e^{2|x|} + 1).
+ * abs err 3.6e-10 before fp32 rounding), else 1 - 2/(e^{2|x|} + 1) (exactly 1 past 9.5).
+ * Both branches are evaluated and one is selected (branch-free, as nn_expf).
  */
 NN_FN float nn_tanhf(float x) {
-    float a = x < 0.0f ? -x : x;
-    float y;
-    if (a < 0.6f) {
-        float u = x * x;
-        float p = 0.0022306744940578938f;
-        p = fmaf(p, u, -0.008266338147222996f);
-        p = fmaf(p, u, 0.021733924746513367f);
-        p = fmaf(p, u, -0.05395231395959854f);
-        p = fmaf(p, u, 0.13333244621753693f);
-        p = fmaf(p, u, -0.3333333134651184f);
-        p = fmaf(p, u, 1.0f);
-        return x * p;
-    }
-    if (a > 9.5f) y = 1.0f;
-    else y = 1.0f - 2.0f / (nn_expf(2.0f * a) + 1.0f);
-    return x < 0.0f ? -y : y;
+    const float a = x < 0.0f ? -x : x;
+    const float u = x * x;
+    float p = 0.0022306744940578938f;
+    p = fmaf(p, u, -0.008266338147222996f);
+    p = fmaf(p, u, 0.021733924746513367f);
+    p = fmaf(p, u, -0.05395231395959854f);
+    p = fmaf(p, u, 0.13333244621753693f);
+    p = fmaf(p, u, -0.3333333134651184f);
+    p = fmaf(p, u, 1.0f);
+    const float small = x * p;
+    float y = 1.0f - 2.0f / (nn_expf(2.0f * a) + 1.0f);
+    y = a > 9.5f ? 1.0f : y;
+    y = x < 0.0f ? -y : y;
+    return a < 0.6f ? small : y;
 }
 
 /*

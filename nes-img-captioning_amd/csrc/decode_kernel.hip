@@ -46,24 +46,35 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 #ifndef DECODE_ABLATE
 #define DECODE_ABLATE 0    // timing-only builds (scripts/ablate.py): 1 no logit epilogue, 2 no stage
-#endif                     // staging, 4 no LSTM cell, 8 no stage-loop barrier -- wrong results
-#ifndef DECODE_PROF
-#define DECODE_PROF 0      // timing-only build: per-wave section cycles written over seq (wrong tokens)
+#endif                     // staging, 8 no stage-loop barrier, 16 no cell activations, 32 no cell
+                           // scratch reads, 64 no early exit -- wrong results
+#if DECODE_ABLATE & 16
+#define CELL_SIG(x) ((x) * 0.5f)
+#define CELL_TANH(x) ((x) * 0.25f)
+#else
+#define CELL_SIG(x) nn_sigmoidf(x)
+#define CELL_TANH(x) nn_tanhf(x)
 #endif
+#ifndef DECODE_PROF
+#define DECODE_PROF 0      // timing-only build: per-workgroup start/end s_memrealtime (100 MHz) of every
+#endif                     // launch written over seq[wg * 4096 + slot] (wrong tokens; scripts/ablate.py)
 #if DECODE_PROF
-#define PROF_STAMP(sec)                                                                          \
+#define PROF_MARK(slot)                                                                          \
     do {                                                                                         \
-        unsigned long long t_;                                                                   \
-        __builtin_amdgcn_sched_barrier(0);                                                       \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                 \
-        __builtin_amdgcn_sched_barrier(0);                                                       \
-        const uint32_t d_ = (uint32_t)(t_ - prof_t0);                                            \
-        _Pragma("unroll") for (int k_ = 0; k_ < 16; ++k_) prof_acc[k_] += prof_cur == k_ ? d_ : 0u;  \
-        prof_t0 = t_;                                                                            \
-        prof_cur = (sec);                                                                        \
+        if (threadIdx.x == 0) {                                                                  \
+            unsigned long long t_, k_;                                                           \
+            asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_), "=s"(k_)::"memory"); \
+            unsigned hw_, xcc_;                                                                  \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                     \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                   \
+            int32_t* q_ = p.seq + (size_t)(blockIdx.x * gridDim.y + blockIdx.y) * 4096;          \
+            q_[(slot)] = (int32_t)(uint32_t)t_;                                                  \
+            q_[2048 + (slot)] = (int32_t)(((xcc_ & 15u) << 16) | ((hw_ >> 8) & 0xffffu));         \
+            q_[1024 + (slot)] = (int32_t)(uint32_t)k_;                                           \
+        }                                                                                        \
     } while (0)
 #else
-#define PROF_STAMP(sec) do { } while (0)
+#define PROF_MARK(slot) do { } while (0)
 #endif
 
 // lane id recomputed at the point of use (volatile: never hoisted or kept live across a loop)
@@ -386,6 +397,7 @@ __device__ __forceinline__ Ctx make_ctx(const DecodeParams& p) {
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParams p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const Ctx c = make_ctx(p);
+    PROF_MARK(80);
     const rsrc_t fc_r = make_rsrc(p.fc, 4u * (uint32_t)p.B * (uint32_t)p.F);
     const uint32_t lo = 4u * c.lane;
     StageRegs sr;
@@ -421,6 +433,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
     st1(c.scr_r, lo, U_SLOT, 1.0f);
     st1(c.scr_r, lo, IT_SLOT, 0.0f);
     if (c.tid == 0) p.alive[c.wg] = 1;
+    PROF_MARK(81);
 }
 
 // ========== LSTM cell of step t (nets.py:98-134): i2h pass + fold ==============================
@@ -431,6 +444,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const Ctx c = make_ctx(p);
     if (t > 0 && p.alive[c.wg] == 0) return;                     // every row finished
+    PROF_MARK(40 + 2 * t);
     const uint32_t lo = 4u * c.lane;
     float xB[64];
     if (t == 0) {
@@ -469,16 +483,21 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
     stage64_store(lds, 64, c.sigma, c.wave * 64 + lane_fresh(), cr);
     __syncthreads();
     f32x16 hold;
-    for (int j = 0; j < 10; ++j) {
+    // unrolled by 5 stages (= 10 gate tiles = 2 unit blocks): which gate each tile holds, and so
+    // which fold it takes, is then known at compile time
+    for (int jo = 0; jo < 10; jo += 5)
+#pragma unroll
+    for (int jj = 0; jj < 5; ++jj) {
+        const int j = jo + jj;
         const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
         const int ma = 2 * j, mb = 2 * j + 1;
         // scratch reads first: vmcnt is in-order, so loads issued after the staging loads would
         // wait for them
         f32x16 pa, pb, cpre;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) pa[r] = ld1(c.scr_r, lo_, P_SLOT(16 * (5 * (ma / 5) + tile_q(ma)) + r));
+        for (int r = 0; r < 16; ++r) pa[r] = (DECODE_ABLATE & 32) ? 0.f : ld1(c.scr_r, lo_, P_SLOT(16 * (5 * (ma / 5) + tile_q(ma)) + r));
 #pragma unroll
-        for (int r = 0; r < 16; ++r) pb[r] = ld1(c.scr_r, lo_, P_SLOT(16 * (5 * (mb / 5) + tile_q(mb)) + r));
+        for (int r = 0; r < 16; ++r) pb[r] = (DECODE_ABLATE & 32) ? 0.f : ld1(c.scr_r, lo_, P_SLOT(16 * (5 * (mb / 5) + tile_q(mb)) + r));
         const int mf = (ma % 5 == 3) ? ma : mb;                  // this stage's f gate, if any
         const bool has_f = (ma % 5 == 3) || (mb % 5 == 3);
 #pragma unroll
@@ -499,11 +518,11 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
                 for (int r = 0; r < 16; ++r) hold[r] = hold[r] > s_[r] ? hold[r] : s_[r];
             } else if (j5 == 2) {                                // ig * g
 #pragma unroll
-                for (int r = 0; r < 16; ++r) hold[r] = nn_sigmoidf(s_[r]) * hold[r];
+                for (int r = 0; r < 16; ++r) hold[r] = CELL_SIG(s_[r]) * hold[r];
             } else if (j5 == 3) {                                // c' = f * c + ig * g
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
-                    const float fcv = nn_sigmoidf(s_[r]) * cpre[r];
+                    const float fcv = CELL_SIG(s_[r]) * cpre[r];
                     const float cn = fcv + hold[r];
                     st1(c.scr_r, lo_, C_SLOT(16 * U + r), cn);
                     hold[r] = cn;
@@ -511,7 +530,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
             } else {                                             // h' = o * tanh(c')
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
-                    st1(c.scr_r, lo_, H_SLOT(16 * U + r), nn_sigmoidf(s_[r]) * nn_tanhf(hold[r]));
+                    st1(c.scr_r, lo_, H_SLOT(16 * U + r), CELL_SIG(s_[r]) * CELL_TANH(hold[r]));
             }
         };
         fold(ma, a0);
@@ -519,6 +538,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
         if (j < 9) stage64_store(lds + ((j + 1) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), cr);
         __syncthreads();
     }
+    PROF_MARK(41 + 2 * t);
 }
 
 // ========== stage kernel of step t: logits + greedy token, then the next cell's h2h sums =======
@@ -531,6 +551,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_stage_kernel(DecodePar
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const Ctx c = make_ctx(p);
     if (t > 0 && p.alive[c.wg] == 0) return;
+    PROF_MARK(2 * (t + 1));
     const uint32_t lo = 4u * c.lane;
     const int nst = (p.V1 + 63) >> 6;
     const int nl = t > 0 ? nst : 0;
@@ -662,9 +683,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_stage_kernel(DecodePar
 #if !DECODE_PROF
         if (c.hh == 0 && c.row_valid) p.seq[(((size_t)c.member * 2 + c.sgn) * p.B + c.b) * p.T + (t - 1)] = it;
 #endif
-        const int any = __syncthreads_or((unfinished && c.row_valid) ? 1 : 0);
+        const int any = __syncthreads_or(((unfinished && c.row_valid) || (DECODE_ABLATE & 64)) ? 1 : 0);
         if (c.tid == 0) p.alive[c.wg] = any;
-        if (!any) return;                                        // no h2h sums needed any more
+        if (!any) { PROF_MARK(2 * (t + 1) + 1); return; }       // no h2h sums needed any more
     }
     // ---- h2h stages: b_h2h + Wh.h of the next step's gate tiles -> lane scratch ------------
     if (nh > 0) {
@@ -687,6 +708,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_stage_kernel(DecodePar
         if (more) stage64_store(lds + ((s + 1) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
         __syncthreads();
     }
+    PROF_MARK(2 * (t + 1) + 1);
 }
 
 extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,

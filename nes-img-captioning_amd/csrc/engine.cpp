@@ -483,6 +483,18 @@ static int opt_step(nicnes_handle* h, int kind, const float* gsum, int32_t P, do
     return NICNES_OK;
 }
 
+int nicnes_last_ratio(nicnes_handle* h, double* ratio_out_host, void* stream) {
+    if (!h || !ratio_out_host) return NICNES_ERR_INVALID;
+    if (h->t == 0) return fail(h, NICNES_ERR_INVALID, "no optimizer step yet");
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    double n2[2];
+    HIPC(h, hipMemcpyAsync(n2, h->norms, sizeof n2, hipMemcpyDeviceToHost, s));
+    HIPC(h, hipStreamSynchronize(s));
+    *ratio_out_host = std::sqrt(n2[0]) / std::sqrt(n2[1]);
+    return NICNES_OK;
+}
+
 int nicnes_adam_step(nicnes_handle* h, const float* gsum, int32_t P, double l2coeff, double stepsize, double beta1,
                      double beta2, double epsilon, double* ratio_out_host, void* stream) {
     if (!h || !gsum || P < 1) return NICNES_ERR_INVALID;

@@ -183,11 +183,20 @@ class Engine:
                                              ctypes.c_float(sigma), _ptr(g), self._stream()), self.h, 'grad_partial')
         return g
 
-    def adam_step(self, gsum, P, l2coeff, stepsize, beta1=0.9, beta2=0.999, epsilon=1e-08):
+    def adam_step(self, gsum, P, l2coeff, stepsize, beta1=0.9, beta2=0.999, epsilon=1e-08, sync=True):
+        """Adam on the engine's theta. sync=True returns the update ratio (one host sync); sync=False
+        only enqueues the step and returns None (read the ratio later with last_ratio())."""
         ratio = ctypes.c_double()
         with torch.cuda.device(self.device):
             check(self.L.nicnes_adam_step(self.h, _ptr(gsum), P, l2coeff, stepsize, beta1, beta2, epsilon,
-                                          ctypes.byref(ratio), self._stream()), self.h, 'adam_step')
+                                          ctypes.byref(ratio) if sync else None, self._stream()), self.h, 'adam_step')
+        return ratio.value if sync else None
+
+    def last_ratio(self):
+        """Update ratio of the newest optimizer step (synchronising)."""
+        ratio = ctypes.c_double()
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_last_ratio(self.h, ctypes.byref(ratio), self._stream()), self.h, 'last_ratio')
         return ratio.value
 
     def sgd_step(self, gsum, P, l2coeff, stepsize, momentum=0.9):

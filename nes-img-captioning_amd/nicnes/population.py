@@ -39,19 +39,22 @@ class PopulationRunner:
             dist.all_gather_into_tensor(self.fit_all, self.fit_local, group=self.group)
         return self.fit_all
 
-    def update(self, iteration):
-        """ranks -> weighted noise sum (local members) -> all-reduce -> Adam. Returns the update ratio."""
+    def update(self, iteration, sync=True):
+        """ranks -> weighted noise sum (local members) -> all-reduce -> Adam. Returns the update ratio
+        (sync=False: nothing waits for the GPU and None is returned; engine.last_ratio() reads it)."""
         _, w = self.e.rank_weights(self.fit_all)
         self.e.grad_partial(iteration, self.m0, self.local, w[self.m0:self.m0 + self.local], self.sigma,
                             out=self.gsum)
         if self.world > 1:
             dist.all_reduce(self.gsum, op=dist.ReduceOp.SUM, group=self.group)
         return self.e.adam_step(self.gsum, self.P, self.l2coeff, self.stepsize, self.beta1, self.beta2,
-                                self.epsilon)
+                                self.epsilon, sync=sync)
 
-    def step(self, iteration):
-        """One full NES iteration. Returns (fitness [P, 2] on device, update ratio)."""
+    def step(self, iteration, sync=True):
+        """One full NES iteration. Returns (fitness [P, 2] on device, update ratio). With sync=False the
+        iteration is only enqueued (ratio None): back-to-back iterations then keep the GPU busy, so
+        its clock does not drop between them."""
         self.evaluate(iteration)
         self.exchange_fitness()
-        ratio = self.update(iteration)
+        ratio = self.update(iteration, sync=sync)
         return self.fit_all, ratio

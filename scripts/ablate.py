@@ -15,12 +15,40 @@ import nicnes  # noqa: E402
 import nicnes.synthetic as S  # noqa: E402
 
 
+def launch_spans(k, seq):
+    """DECODE_PROF=1 build: per-launch span, workgroup durations, per-CU busy time, in-kernel clock."""
+    raw = seq.reshape(-1, 4096).cpu().numpy().astype(np.int64) & 0xffffffff
+    ts, cyc, hw = raw[:, :1024], raw[:, 1024:2048], raw[:, 2048:]
+    launches = [('img', 80)] + [('stage%d' % t, 2 * (t + 1)) for t in range(-1, 17)] + \
+               [('cell%d' % t, 40 + 2 * t) for t in range(0, 17)]
+    t0 = ts[:, 80].min()
+    rows = []
+    for name, sl in launches:
+        st = (ts[:, sl] - t0) % (1 << 32)
+        en = (ts[:, sl + 1] - t0) % (1 << 32)
+        dur = (en - st) / 100.0                               # us (100 MHz counter)
+        ghz = np.median(((cyc[:, sl + 1] - cyc[:, sl]) % (1 << 32)) / np.maximum(dur, 1e-3) / 1e3)
+        span = (en.max() - st.min()) / 100.0
+        per_cu = {}
+        for c_, d_ in zip(hw[:, sl], dur):
+            per_cu[c_] = per_cu.get(c_, 0.0) + d_
+        busy = np.array(list(per_cu.values()))
+        rows.append((name, st.min() / 100.0, span, dur.mean(), dur.min(), dur.max(), len(per_cu),
+                     busy.mean(), busy.max(), busy.mean() / span, ghz))
+    print(k, 'launch: start_us span_us wg_mean wg_min wg_max n_cu cu_busy_mean cu_busy_max eff(mean busy/span) GHz')
+    for r in sorted(rows, key=lambda r: r[1]):
+        print('%-8s %9.1f %8.1f %8.1f %8.1f %8.1f %4d %8.1f %8.1f %6.3f %5.2f' % r)
+
+
 def main():
     pop = int(os.environ.get('POP', '512'))
     rounds = int(os.environ.get('ROUNDS', '3'))
     libs = sorted(glob.glob(os.path.join(REPO, 'nes-img-captioning_amd', 'build', 'ablate', 'libnicnes_*.so')))
     noise = torch.from_numpy(S.noise_table(1 << 27)).cuda()
     engines = {}
+    only = [x for x in os.environ.get('ONLY', '').split(',') if x]
+    if only:
+        libs = [p for p in libs if os.path.basename(p)[len('libnicnes_'):-3] in only + ['base']]
     libs.sort(key=lambda p: not p.endswith('_base.so'))          # base first: it makes the refs
     wl = None
     for path in libs:
@@ -37,30 +65,41 @@ def main():
         e.set_timing(True)
         engines[name] = e
     res = {k: [] for k in engines}
+    phase = {k: [] for k in engines}
     for r in range(rounds):
         for k, e in engines.items():
             e.evaluate(r + 1, 0, pop, 0.01)
             res[k].append(e.kernel_times()[0])
+            phase[k].append(e.decode_phase_times())
     ref = engines['base'].evaluate(99, 0, 8, 0.01, return_seq=True)
     for k in [x for x in os.environ.get('EXACT', '').split(',') if x]:   # variants that must match base
         if k in engines:
             got = engines[k].evaluate(99, 0, 8, 0.01, return_seq=True)
             print(k, 'tokens == base:', bool(torch.equal(got[1], ref[1])), 'fitness == base:',
                   bool(torch.equal(got[0], ref[0])))
-    for k in [x for x in engines if x.startswith('prof')]:   # DECODE_PROF builds: section cycles
-        _, seq = engines[k].evaluate(50, 0, pop, 0.01, return_seq=True)
-        cyc = seq.view(pop, -1)[:, :128].reshape(pop, 8, 16).double().cpu().numpy()   # [member, wave, section]
-        names = ['img', 'embed', 'cell_p1', 'cell_p2', 'cell_elem', 'logit', 'finish', 'tail', 'lg_issue',
-                 'lg_mfma_epi', 'lg_store_or_wait', 'lg_barrier', 'lg_form', 's13', 's14', 's15']
-        tot = cyc.sum(axis=2).mean()
-        print(k, 'mean cycles per wave:', json.dumps({n: round(float(cyc[:, :, i].mean()), 0) for i, n in enumerate(names)}),
-              'total', round(float(tot), 0), 'frac', json.dumps({n: round(float(cyc[:, :, i].mean() / tot), 4)
-                                                                   for i, n in enumerate(names)}))
-        for i in (5, 8, 9, 10, 11, 12):
-            print(k, names[i], 'sgn0 %.0f sgn1 %.0f' % (cyc[:, :4, i].mean(), cyc[:, 4:, i].mean()))
+    for k in [x for x in engines if x.startswith('prof')]:   # DECODE_PROF builds: per-WG launch spans
+        torch.cuda.synchronize()
+        time.sleep(0.05)
+        e = engines[k]
+        seqs = []
+        gsum = torch.empty(e.D, dtype=torch.float32, device='cuda')
+        for q in range(3):                      # bench-like iterations, nothing waits in between
+            fit, seq = e.evaluate(50 + q, 0, pop, 0.01, return_seq=True)
+            _, w = e.rank_weights(fit)
+            e.grad_partial(50 + q, 0, pop, w, 0.01, out=gsum)
+            e.adam_step(gsum, pop, 1e-7, 1e-6, sync=False)
+            seqs.append(seq)
+        for q, seq in enumerate(seqs):
+            print('--- %s iteration %d of 3 (decode, CIDEr-D, ranks, noise sum, Adam), queued after a 50 ms idle'
+                  % (k, q + 1))
+            launch_spans(k, seq)
     base = np.median(res['base'])
     out = {k: {'median_ms': round(float(np.median(v)), 3), 'min_ms': round(float(np.min(v)), 3),
-               'vs_base': round(float(np.median(v) / base), 3)} for k, v in res.items()}
+               'vs_base': round(float(np.median(v) / base), 3),
+               'stage_ms': round(float(np.median([ph['stage_ms'] for ph in phase[k]])), 3),
+               'cell_ms': round(float(np.median([ph['cell_ms'] for ph in phase[k]])), 3),
+               'img_ms': round(float(np.median([ph['img_ms'] for ph in phase[k]])), 3),
+               'tie_fallbacks': engines[k].stats()['tie_fallbacks']} for k, v in res.items()}
     print(json.dumps(out, indent=1))
 
 

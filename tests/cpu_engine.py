@@ -85,13 +85,17 @@ class OracleEngine:
             return out
         return g
 
-    def adam_step(self, gsum, P, l2coeff, stepsize, beta1=0.9, beta2=0.999, epsilon=1e-08):
+    def adam_step(self, gsum, P, l2coeff, stepsize, beta1=0.9, beta2=0.999, epsilon=1e-08, sync=True):
         if self.adam is None:
             self.adam = O.AdamOracle(self.theta_src.copy(), stepsize, beta1, beta2, epsilon)
         g = gsum.numpy().astype(np.float32) / np.float32(2 * P)
         ratio, theta = O.master_update(self.adam, g, l2coeff)
         self.theta32 = np.asarray(theta).astype(np.float32)
-        return float(ratio)
+        self._ratio = float(ratio)
+        return self._ratio if sync else None
+
+    def last_ratio(self):
+        return self._ratio
 
 
 def tiny_workload(B=4, seed=0):
