@@ -294,11 +294,13 @@ __device__ __forceinline__ void row_state_init(RowState& st) {
 // earliest record (left-to-right maximum) inside the log_softmax tie window of the final max;
 // each lane half keeps its last two records and the largest record it evicted, so an
 // overflowing row is detected and decoded by the exact pass.
-__device__ __forceinline__ void records16(RowState& st, const f32x16& P, int vbase) {
+// records4: the record update over P[4k .. 4k+3] (vocab vbase + 8k + 0..3, in index order)
+template <int K>
+__device__ __forceinline__ void records4(RowState& st, const f32x16& P, int vbase) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const float L = P[r];
-        const int v = vbase + (r & 3) + 8 * (r >> 2);
+    for (int e = 0; e < 4; ++e) {
+        const float L = P[4 * K + e];
+        const int v = vbase + 8 * K + e;
         const bool c = L > st.r1v;
         st.ev = c ? st.r0v : st.ev;
         st.r0v = c ? st.r1v : st.r0v;
@@ -308,17 +310,18 @@ __device__ __forceinline__ void records16(RowState& st, const f32x16& P, int vba
     }
 }
 
-// epilogue of one logit stage: P0 holds vocab vbase + (r&3) + 8(r>>2), P1 the same + 32. Record
-// scans run only in the (wave-uniform) case that some lane sees a new running max.
+__device__ __forceinline__ float max4(const f32x16& P, int k) {
+    return fmaxf(fmaxf(fmaxf(P[4 * k], P[4 * k + 1]), P[4 * k + 2]), P[4 * k + 3]);
+}
+
+// epilogue of one logit stage: P0 holds vocab vbase + (r&3) + 8(r>>2), P1 the same + 32.
+// Record scans run per group of 4 consecutive vocab ids, only in the (wave-uniform) case that
+// some lane sees a new running max in that group: a wave covers 32 rows, so whole-stage scans
+// would run in most stages, while a group scan is needed in few once the running max settles.
 __device__ __forceinline__ void epilogue64(RowState& st, const f32x16& P0, const f32x16& P1, int vbase) {
-    float t0 = fmaxf(fmaxf(P0[0], P0[1]), P0[2]);
-    float t1 = fmaxf(fmaxf(P1[0], P1[1]), P1[2]);
-#pragma unroll
-    for (int r = 3; r < 15; r += 2) {
-        t0 = fmaxf(fmaxf(t0, P0[r]), P0[r + 1]);
-        t1 = fmaxf(fmaxf(t1, P1[r]), P1[r + 1]);
-    }
-    const float tmax = fmaxf(fmaxf(t0, P0[15]), fmaxf(t1, P1[15]));
+    const float g0 = max4(P0, 0), g1 = max4(P0, 1), g2 = max4(P0, 2), g3 = max4(P0, 3);
+    const float g4 = max4(P1, 0), g5 = max4(P1, 1), g6 = max4(P1, 2), g7 = max4(P1, 3);
+    const float tmax = fmaxf(fmaxf(fmaxf(g0, g1), fmaxf(g2, g3)), fmaxf(fmaxf(g4, g5), fmaxf(g6, g7)));
     const float mnew = fmaxf(st.m, tmax);
     const float ml = mnew * LOG2E;
     float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
@@ -329,8 +332,14 @@ __device__ __forceinline__ void epilogue64(RowState& st, const f32x16& P0, const
     st.s = s;
     st.m = mnew;
     if (__any(tmax > st.r1v)) {
-        records16(st, P0, vbase);
-        records16(st, P1, vbase + 32);
+        if (__any(g0 > st.r1v)) records4<0>(st, P0, vbase);
+        if (__any(g1 > st.r1v)) records4<1>(st, P0, vbase);
+        if (__any(g2 > st.r1v)) records4<2>(st, P0, vbase);
+        if (__any(g3 > st.r1v)) records4<3>(st, P0, vbase);
+        if (__any(g4 > st.r1v)) records4<0>(st, P1, vbase + 32);
+        if (__any(g5 > st.r1v)) records4<1>(st, P1, vbase + 32);
+        if (__any(g6 > st.r1v)) records4<2>(st, P1, vbase + 32);
+        if (__any(g7 > st.r1v)) records4<3>(st, P1, vbase + 32);
     }
 }
 
@@ -483,12 +492,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
     stage64_store(lds, 64, c.sigma, c.wave * 64 + lane_fresh(), cr);
     __syncthreads();
     f32x16 hold;
-    // unrolled by 5 stages (= 10 gate tiles = 2 unit blocks): which gate each tile holds, and so
-    // which fold it takes, is then known at compile time
-    for (int jo = 0; jo < 10; jo += 5)
-#pragma unroll
-    for (int jj = 0; jj < 5; ++jj) {
-        const int j = jo + jj;
+    for (int j = 0; j < 10; ++j) {
         const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
         const int ma = 2 * j, mb = 2 * j + 1;
         // scratch reads first: vmcnt is in-order, so loads issued after the staging loads would
