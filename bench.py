@@ -35,11 +35,10 @@ def decode_flops_per_member(B, V1=9488, E=128, R=128, F=2048):
     return 2 * B * per_row
 
 
-def stage_flops_per_member(B, V1=9488, E=128, R=128):
-    """The part of decode_flops_per_member done by nicnes_decode_stage_kernel: the 16 logit GEMMs
-    and the 17 h2h halves of the gate sums (the cell kernel does the i2h halves, the img kernel
-    the image projection)."""
-    per_row = 2 * (17 * (R * 5 * R) + 16 * (R * V1))
+def step_flops_per_member(B, V1=9488, E=128, R=128):
+    """The part of decode_flops_per_member done by nicnes_decode_step_kernel: the 16 logit GEMMs and
+    the 17 LSTM cells' gate sums, i2h and h2h halves (the img kernel does the image projection)."""
+    per_row = 2 * (17 * (2 * E * 5 * R) + 16 * (R * V1))
     return 2 * B * per_row
 
 
@@ -140,18 +139,19 @@ def main():
     value = P * args.steps / dt
     dec_s = float(np.mean(dec_ms)) / 1e3
     flops = decode_flops_per_member(B) * P_local
-    # dominant kernel: the logit/h2h stage kernel, T + 2 launches per evaluate; per-launch figures
-    # are the evaluate's totals / launches (what rocprofv3 --stats averages over the same launches)
-    n_stage = phases[-1]['stage_launches']
-    stage_ms = float(np.mean([ph['stage_ms'] for ph in phases])) / n_stage
-    stage_flop = stage_flops_per_member(B) * P_local / n_stage
-    achieved = stage_flop / (stage_ms / 1e3) / 1e12
+    # dominant kernel: the step kernel (logits + token + next LSTM cell), T + 2 launches per
+    # evaluate; per-launch figures are the evaluate's totals / launches (what rocprofv3 --stats
+    # averages over the same launches)
+    n_step = phases[-1]['step_launches']
+    step_ms = float(np.mean([ph['step_ms'] for ph in phases])) / n_step
+    step_flop = step_flops_per_member(B) * P_local / n_step
+    achieved = step_flop / (step_ms / 1e3) / 1e12
     traffic = None
     pmc = os.path.join(REPO, 'profiles', 'r01_decode_pmc.json')
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
-        if rec.get('kernel') == 'nicnes_decode_stage_kernel':
+        if rec.get('kernel') == 'nicnes_decode_step_kernel':
             traffic = rec.get('hbm_bytes_per_launch')
     out = {
         'metric': METRIC, 'value': round(value, 3), 'unit': 'members/s', 'n_gpus': world, 'steps': args.steps,
@@ -164,17 +164,17 @@ def main():
                    'population': P, 'members_per_gpu': P_local, 'batch_size': B, 'seq_length': 16,
                    'vocab_size': 9487, 'parallelism': 'population-sharded x%d, RCCL all-gather + all-reduce'
                    % world},
-        'roofline': {'bound': 'mfma', 'kernel': 'nicnes_decode_stage_kernel', 'achieved': round(achieved, 3),
+        'roofline': {'bound': 'mfma', 'kernel': 'nicnes_decode_step_kernel', 'achieved': round(achieved, 3),
                      'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                      'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,
-                     'kernel_ms_per_launch': round(stage_ms, 4), 'launches_per_step': n_stage,
-                     'algorithmic_flop_per_launch': stage_flop,
+                     'kernel_ms_per_launch': round(step_ms, 4), 'launches_per_step': n_step,
+                     'algorithmic_flop_per_launch': step_flop,
                      'decode': {'ms_per_step': round(dec_s * 1e3, 3), 'algorithmic_flop': flops,
                                 'tflops': round(flops / dec_s / 1e12, 3),
                                 'frac': round(flops / dec_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
                                 'img_ms': round(float(np.mean([ph['img_ms'] for ph in phases])), 3),
-                                'cell_ms': round(float(np.mean([ph['cell_ms'] for ph in phases])), 3),
-                                'stage_ms': round(stage_ms * n_stage, 3)}},
+                                'cell_only_ms': round(float(np.mean([ph['cell_only_ms'] for ph in phases])), 3),
+                                'step_ms': round(step_ms * n_step, 3)}},
         'cpu_baseline': cpu,
         'tie_fallbacks': eng.stats()['tie_fallbacks'],
         'update_ratio': ratio,

@@ -134,8 +134,8 @@ int nicnes_set_timing(nicnes_handle* h, int on);
 int nicnes_kernel_times(nicnes_handle* h, float* out2_host);
 
 /* Per-kernel split of the last timed decode (events between its launches): [0] = img-embed kernel
- * ms, [1] = the T+1 LSTM-cell launches summed, [2] = the T+2 logit/h2h stage launches summed,
- * [3] = the number of stage launches. Synchronising. */
+ * ms, [1] = the two cell-only step launches (t = -1, 0) summed, [2] = all T+2 step launches
+ * (logits + token + next cell) summed, [3] = the number of step launches. Synchronising. */
 int nicnes_decode_phase_times(nicnes_handle* h, float* out4_host);
 
 #ifdef __cplusplus

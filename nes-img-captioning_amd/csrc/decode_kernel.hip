@@ -15,11 +15,11 @@
 // fp32(W0 +/- fp32(sigma * z[idx + offset])) from the base theta and the member's noise slice,
 // once for both signs.
 //
-// Step structure. LSTMCore forms all_input_sums = i2h(x) + h2h(h) (nets.py:109-111). The h2h
-// half only needs h, which is the B operand of the logit GEMM of the same step, so its 640 gate
-// rows run as 10 extra 64-row stages of the logit stage loop, and their sums go to lane scratch.
-// Once the token is known, the i2h pass (10 stages over x = embed(token)) adds them and folds the
-// LSTM cell per 32-unit block as the gates complete (order g1, g2, i, f, o).
+// Step structure. One launch per step (nicnes_decode_step_kernel): the logit GEMM of step t over
+// h_t, the greedy token, then the LSTM cell of step t+1, whose gate sums i2h(x) + h2h(h)
+// (nets.py:109-111) use h_t while it is still the live B operand. The cell runs as 20 stages, one
+// per 32-unit gate tile (i2h rows | h2h rows), folded per unit block as the gates complete (order
+// g1, g2, i, f, o); only c' and h' cross to the next launch, in lane scratch.
 //
 // Addressing: every global access goes through a buffer resource (wave-uniform 128-bit
 // descriptor + 32-bit lane offset) so no 64-bit VGPR address pairs are kept live. Lane-derived
@@ -42,12 +42,11 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #define STAGE64_FLOATS (2 * 64 * LDS_ROW + 128)       // 64-row stage: W+ | W- | bias+ (64) | bias- (64)
 #define LOG2E 1.44269504088896340736f
 #define NEG_INF (-__builtin_inff())
-#define H2H_STAGES 10                                 // 640 gate rows / 64
 
 #ifndef DECODE_ABLATE
 #define DECODE_ABLATE 0    // timing-only builds (scripts/ablate.py): 1 no logit epilogue, 2 no stage
-#endif                     // staging, 8 no stage-loop barrier, 16 no cell activations, 32 no cell
-                           // scratch reads, 64 no early exit -- wrong results
+#endif                     // staging, 8 no stage-loop barrier, 16 no cell activations, 64 no early
+                           // exit -- wrong results
 #if DECODE_ABLATE & 16
 #define CELL_SIG(x) ((x) * 0.5f)
 #define CELL_TANH(x) ((x) * 0.25f)
@@ -274,6 +273,34 @@ __device__ __forceinline__ void mfma_stage64(const float* w, const float* bias, 
     }
 }
 
+// cell stage: chain a = i2h tile (stage rows 0-31) over B = x, chain b = h2h tile (rows 32-63)
+// over B = h; k chunks [T0, T1) of 32 (init: start from the bias)
+template <int T0, int T1>
+__device__ __forceinline__ void mfma_xh_part(const float* w, const float* bias, const float (&Bx)[64],
+                                             const float (&Bh)[64], int lane, f32x16& acc0, f32x16& acc1) {
+    const int hh = lane >> 5;
+    const float* row0 = w + (lane & 31) * LDS_ROW + hh * 16;
+    const float* row1 = row0 + 32 * LDS_ROW;
+    if (T0 == 0) {
+        acc0 = bias_init(bias, hh);
+        acc1 = bias_init(bias + 32, hh);
+    }
+#pragma unroll
+    for (int T = T0; T < T1; ++T) {
+        f32x4 a0[4], a1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            a0[c] = *reinterpret_cast<const f32x4*>(row0 + T * 32 + 4 * c);
+            a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bx[16 * T + jj], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bh[16 * T + jj], acc1, 0, 0, 0);
+        }
+    }
+}
+
 // ---- per-row greedy state over the vocabulary (log_softmax + first argmax, nets.py:202,208) --
 struct RowState {
     float m;              // running max logit (== newest record)
@@ -361,15 +388,12 @@ __device__ __forceinline__ int tile_q(int m) { const int j = m % 5; return j < 2
 __device__ __forceinline__ uint32_t gate_row(int m) { return (uint32_t)(tile_q(m) * 128 + 32 * (m / 5)); }
 
 // ---- the kernels ------------------------------------------------------------------------------
-// One evaluate = img, stage(-1), then per step t = 0..T: cell(t), stage(t). Separate launches give
-// each phase its own register allocation (x and h are never live together); state between them
-// is lane-private scratch plus a per-workgroup `alive` flag (nets.py:242-243 early exit).
+// One evaluate = img, then step(t) for t = -1..T. State between launches is lane-private scratch
+// plus a per-workgroup `alive` flag (nets.py:242-243 early exit).
 #define C_SLOT(s) (4u * 64u * (uint32_t)(s))            // c
 #define H_SLOT(s) (4u * 64u * (uint32_t)(64 + (s)))     // h'
-#define P_SLOT(s) (4u * 64u * (uint32_t)(128 + (s)))    // 20 h2h gate-sum tiles
-#define X_SLOT(s) (4u * 64u * (uint32_t)(448 + (s)))    // x of t = 0 (img_embed)
-#define U_SLOT (4u * 64u * 512u)                        // row unfinished (1.0 / 0.0)
-#define IT_SLOT (4u * 64u * 513u)                       // last emitted token of the row
+#define X_SLOT(s) (4u * 64u * (uint32_t)(128 + (s)))    // x of t = 0 (img_embed)
+#define U_SLOT (4u * 64u * 192u)                        // row unfinished (1.0 / 0.0)
 
 struct Ctx {
     int tid, lane, wave, sgn, grp, hh, member, slab, b, bc, wg;
@@ -440,118 +464,22 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
 #pragma unroll
         for (int r = 0; r < 16; ++r) st1(c.scr_r, lo, X_SLOT(16 * U + r), accU[U][r]);
     st1(c.scr_r, lo, U_SLOT, 1.0f);
-    st1(c.scr_r, lo, IT_SLOT, 0.0f);
     if (c.tid == 0) p.alive[c.wg] = 1;
     PROF_MARK(81);
 }
 
-// ========== LSTM cell of step t (nets.py:98-134): i2h pass + fold ==============================
-// s = (b_i2h + Wi.x) + (b_h2h + Wh.h): the h2h half was stored by the previous stage kernel.
-// Stage j holds gate tiles 2j, 2j+1 (tile_q order); the gates of unit block U are folded with
-// nn_lstm_cell's operations, in its order, as they complete.
-__global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodeParams p, int t) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const Ctx c = make_ctx(p);
-    if (t > 0 && p.alive[c.wg] == 0) return;                     // every row finished
-    PROF_MARK(40 + 2 * t);
-    const uint32_t lo = 4u * c.lane;
-    float xB[64];
-    if (t == 0) {
-#pragma unroll
-        for (int i = 0; i < 64; ++i) xB[i] = ld1(c.scr_r, lo, X_SLOT(i));
-    } else {                                                     // x = embed(it) (nets.py:196-199)
-        const int it = (int)ld1(c.scr_r, lo, IT_SLOT);
-        const uint32_t eo = 4u * ((uint32_t)p.off_emb_w + (uint32_t)it * 128u + 4u * c.hh);
-#pragma unroll
-        for (int T = 0; T < 4; ++T)
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                const f32x4 w = ld4(c.theta_r, eo + 4u * (32 * T + 8 * a));
-                const f32x4 z = ld4(c.noise_r, eo + 4u * (32 * T + 8 * a));
-                const f32x4 delta = c.sigma * z;
-                const f32x4 x = c.sgn ? (w - delta) : (w + delta);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) xB[16 * T + 4 * a + e] = x[e];
-            }
-    }
-#pragma unroll
-    for (int i = 0; i < 64; ++i) pin(xB[i]);
-    auto cell_src = [&](int j) {
-        const uint32_t ra = gate_row(2 * j), rb = gate_row(2 * j + 1), rm = min(ra, rb);
-        StageSrc S;
-        S.w_r = c.theta_r; S.z_r = c.noise_r; S.b_r = c.theta_r; S.bz_r = c.noise_r;
-        S.so_a = 4u * ((uint32_t)p.off_i2h_w + 128u * ra);
-        S.so_b = 4u * ((uint32_t)p.off_i2h_w + 128u * rb);
-        S.bso = 4u * ((uint32_t)p.off_i2h_b + rm);
-        S.bda = 4u * (ra - rm); S.bdb = 4u * (rb - rm);
-        S.valid = 64;
-        return S;
-    };
-    Stage64Regs cr;
-    stage64_load(cell_src(0), c.wave * 64 + lane_fresh(), cr);
-    stage64_store(lds, 64, c.sigma, c.wave * 64 + lane_fresh(), cr);
-    __syncthreads();
-    f32x16 hold;
-    for (int j = 0; j < 10; ++j) {
-        const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
-        const int ma = 2 * j, mb = 2 * j + 1;
-        // scratch reads first: vmcnt is in-order, so loads issued after the staging loads would
-        // wait for them
-        f32x16 pa, pb, cpre;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) pa[r] = (DECODE_ABLATE & 32) ? 0.f : ld1(c.scr_r, lo_, P_SLOT(16 * (5 * (ma / 5) + tile_q(ma)) + r));
-#pragma unroll
-        for (int r = 0; r < 16; ++r) pb[r] = (DECODE_ABLATE & 32) ? 0.f : ld1(c.scr_r, lo_, P_SLOT(16 * (5 * (mb / 5) + tile_q(mb)) + r));
-        const int mf = (ma % 5 == 3) ? ma : mb;                  // this stage's f gate, if any
-        const bool has_f = (ma % 5 == 3) || (mb % 5 == 3);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) cpre[r] = (has_f && t > 0) ? ld1(c.scr_r, lo_, C_SLOT(16 * (mf / 5) + r)) : 0.f;
-        __builtin_amdgcn_sched_barrier(0);
-        if (j < 9) stage64_load(cell_src(j + 1), c.wave * 64 + lane_fresh(), cr);
-        const float* buf = lds + (j & 1) * STAGE64_FLOATS;
-        f32x16 a0, a1;
-        mfma_stage64(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, lane_fresh(), a0, a1);
-        a0 = a0 + pa;                                            // i2h(x) + h2h(h), nets.py:109-111
-        a1 = a1 + pb;
-        auto fold = [&](int m, const f32x16& s_) {
-            const int U = m / 5, j5 = m % 5;
-            if (j5 == 0) {                                       // g1
-                hold = s_;
-            } else if (j5 == 1) {                                // g = max(g1, g2)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) hold[r] = hold[r] > s_[r] ? hold[r] : s_[r];
-            } else if (j5 == 2) {                                // ig * g
-#pragma unroll
-                for (int r = 0; r < 16; ++r) hold[r] = CELL_SIG(s_[r]) * hold[r];
-            } else if (j5 == 3) {                                // c' = f * c + ig * g
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float fcv = CELL_SIG(s_[r]) * cpre[r];
-                    const float cn = fcv + hold[r];
-                    st1(c.scr_r, lo_, C_SLOT(16 * U + r), cn);
-                    hold[r] = cn;
-                }
-            } else {                                             // h' = o * tanh(c')
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    st1(c.scr_r, lo_, H_SLOT(16 * U + r), CELL_SIG(s_[r]) * CELL_TANH(hold[r]));
-            }
-        };
-        fold(ma, a0);
-        fold(mb, a1);
-        if (j < 9) stage64_store(lds + ((j + 1) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), cr);
-        __syncthreads();
-    }
-    PROF_MARK(41 + 2 * t);
-}
-
-// ========== stage kernel of step t: logits + greedy token, then the next cell's h2h sums =======
-// stages [0, nl): logit rows 64s.. (nets.py:202); then nh h2h stages: b_h2h + Wh.h of the next
-// step's gate tiles, stored to lane scratch. t = -1 runs only the h2h stages over h = 0. In the
-// logit loop the two waves sharing a SIMD (w and w+4: opposite signs) run the MFMA chains and the
-// VALU epilogue of the previous stage in opposite orders, so VALU of one wave overlaps the MFMAs
-// of the other.
-__global__ __launch_bounds__(NTHREADS) void nicnes_decode_stage_kernel(DecodeParams p, int t) {
+// ========== step kernel: logits + greedy token of step t, then the LSTM cell of step t+1 ========
+// One launch per step t = -1 .. T. Logits (nets.py:202,208-209) run for t >= 1 over h = h_t (t = 0
+// is the image step, whose output the reference discards). The cell of step t+1 (nets.py:98-134)
+// follows in the same launch while h_t is still the live B operand: its gate sums
+// s = (b_i2h + Wi.x) + (b_h2h + Wh.h) run as 20 stages, one per 32-unit gate tile, each staging
+// the tile's i2h rows (chain a, B = x = embed(token), nets.py:196-199, or img_embed(fc) at t = -1)
+// and its h2h rows (chain b, B = h). The tiles come in nn_lstm_cell's fold order per unit block
+// (g1, g2, i, f, o), so c' and h' are folded in registers as the gates complete; only c' and h'
+// go to lane scratch. In the logit loop the two waves sharing a SIMD (w and w+4: opposite signs)
+// run the MFMA chains and the VALU epilogue of the previous stage in opposite orders, so VALU of
+// one wave overlaps the MFMAs of the other.
+__global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodeParams p, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const Ctx c = make_ctx(p);
     if (t > 0 && p.alive[c.wg] == 0) return;
@@ -559,13 +487,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_stage_kernel(DecodePar
     const uint32_t lo = 4u * c.lane;
     const int nst = (p.V1 + 63) >> 6;
     const int nl = t > 0 ? nst : 0;
-    const int nh = t < p.T ? H2H_STAGES : 0;
-    const int ns = nl + nh;
     const uint64_t nidx = p.noise_idx[c.member];
-    const rsrc_t lw_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
-    const rsrc_t lz_r = make_rsrc(p.noise + nidx + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
-    const rsrc_t lbw_r = make_rsrc(p.theta + p.off_log_b, 4u * (uint32_t)p.V1);
-    const rsrc_t lbz_r = make_rsrc(p.noise + nidx + p.off_log_b, 4u * (uint32_t)p.V1);
     float hB[64];
     if (t < 0) {
 #pragma unroll
@@ -576,29 +498,23 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_stage_kernel(DecodePar
     }
 #pragma unroll
     for (int i = 0; i < 64; ++i) pin(hB[i]);
-    auto lsrc = [&](int s) {                                     // logit rows 64s .. 64s+63
-        StageSrc S;
-        S.w_r = lw_r; S.z_r = lz_r; S.b_r = lbw_r; S.bz_r = lbz_r;
-        S.so_a = 32768u * (uint32_t)s; S.so_b = S.so_a + 16384u;
-        S.bso = 256u * (uint32_t)s; S.bda = 0u; S.bdb = 128u;
-        S.valid = p.V1 - 64 * s;
-        return S;
-    };
-    auto hsrc = [&](int jh) {                                    // h2h gate tiles 2jh, 2jh+1
-        StageSrc S;
-        const uint32_t ra = gate_row(2 * jh), rb = gate_row(2 * jh + 1), rm = min(ra, rb);
-        S.w_r = c.theta_r; S.z_r = c.noise_r; S.b_r = c.theta_r; S.bz_r = c.noise_r;
-        S.so_a = 4u * ((uint32_t)p.off_h2h_w + 128u * ra);
-        S.so_b = 4u * ((uint32_t)p.off_h2h_w + 128u * rb);
-        S.bso = 4u * ((uint32_t)p.off_h2h_b + rm);
-        S.bda = 4u * (ra - rm); S.bdb = 4u * (rb - rm);
-        S.valid = 64;
-        return S;
-    };
     Stage64Regs s64;
-    RowState st;
-    row_state_init(st);
+    int it = 0;                                   // token fed to the next cell (0 = BOS at t = 0)
     if (nl > 0) {
+        const rsrc_t lw_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
+        const rsrc_t lz_r = make_rsrc(p.noise + nidx + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
+        const rsrc_t lbw_r = make_rsrc(p.theta + p.off_log_b, 4u * (uint32_t)p.V1);
+        const rsrc_t lbz_r = make_rsrc(p.noise + nidx + p.off_log_b, 4u * (uint32_t)p.V1);
+        auto lsrc = [&](int s) {                                 // logit rows 64s .. 64s+63
+            StageSrc S;
+            S.w_r = lw_r; S.z_r = lz_r; S.b_r = lbw_r; S.bz_r = lbz_r;
+            S.so_a = 32768u * (uint32_t)s; S.so_b = S.so_a + 16384u;
+            S.bso = 256u * (uint32_t)s; S.bda = 0u; S.bdb = 128u;
+            S.valid = p.V1 - 64 * s;
+            return S;
+        };
+        RowState st;
+        row_state_init(st);
         stage64_load(lsrc(0), c.wave * 64 + lane_fresh(), s64);
         stage64_store(lds, lsrc(0).valid, c.sigma, c.wave * 64 + lane_fresh(), s64);
         __syncthreads();
@@ -681,35 +597,98 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_stage_kernel(DecodePar
         if (tok >= p.V1) tok = 0;
         // finished mask (nets.py:236-243)
         const bool unfinished = ld1(c.scr_r, lo, U_SLOT) != 0.f && tok > 0;
-        const int it = unfinished ? tok : 0;
+        it = unfinished ? tok : 0;
         st1(c.scr_r, lo, U_SLOT, unfinished ? 1.f : 0.f);
-        st1(c.scr_r, lo, IT_SLOT, (float)it);
 #if !DECODE_PROF
         if (c.hh == 0 && c.row_valid) p.seq[(((size_t)c.member * 2 + c.sgn) * p.B + c.b) * p.T + (t - 1)] = it;
 #endif
         const int any = __syncthreads_or(((unfinished && c.row_valid) || (DECODE_ABLATE & 64)) ? 1 : 0);
         if (c.tid == 0) p.alive[c.wg] = any;
-        if (!any) { PROF_MARK(2 * (t + 1) + 1); return; }       // no h2h sums needed any more
+        if (!any) { PROF_MARK(2 * (t + 1) + 1); return; }       // the reference stops here (nets.py:242-243)
     }
-    // ---- h2h stages: b_h2h + Wh.h of the next step's gate tiles -> lane scratch ------------
-    if (nh > 0) {
-        stage64_load(hsrc(0), c.wave * 64 + lane_fresh(), s64);
-        stage64_store(lds + (nl & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
-        __syncthreads();
+    if (t >= p.T) { PROF_MARK(2 * (t + 1) + 1); return; }
+
+    // ---- LSTM cell of step t+1 ---------------------------------------------------------------
+    float xB[64];
+    if (t < 0) {                                                 // x = img_embed(fc) (nets.py:194-195)
+#pragma unroll
+        for (int i = 0; i < 64; ++i) xB[i] = ld1(c.scr_r, lo, X_SLOT(i));
+    } else {                                                     // x = embed(it) (nets.py:196-199)
+        const uint32_t eo = 4u * ((uint32_t)p.off_emb_w + (uint32_t)it * 128u + 4u * c.hh);
+#pragma unroll
+        for (int T = 0; T < 4; ++T)
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const f32x4 w = ld4(c.theta_r, eo + 4u * (32 * T + 8 * a));
+                const f32x4 z = ld4(c.noise_r, eo + 4u * (32 * T + 8 * a));
+                const f32x4 delta = c.sigma * z;
+                const f32x4 x = c.sgn ? (w - delta) : (w + delta);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) xB[16 * T + 4 * a + e] = x[e];
+            }
     }
-    for (int s = nl; s < ns; ++s) {
-        const bool more = s + 1 < ns;
-        if (more) stage64_load(hsrc(s + 1 - nl), c.wave * 64 + lane_fresh(), s64);
-        const float* buf = lds + (s & 1) * STAGE64_FLOATS;
-        f32x16 acc0, acc1;
-        mfma_stage64(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, hB, lane_fresh(), acc0, acc1);
-        const int jh = s - nl, ma = 2 * jh, mb = 2 * jh + 1;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) pin(xB[i]);
+    const uint32_t ib = (uint32_t)p.off_i2h_b, hb = (uint32_t)p.off_h2h_b, bmin = min(ib, hb);
+    auto csrc = [&](int m) {                                     // gate tile m: i2h rows | h2h rows
+        const uint32_t r = gate_row(m);
+        StageSrc S;
+        S.w_r = c.theta_r; S.z_r = c.noise_r; S.b_r = c.theta_r; S.bz_r = c.noise_r;
+        S.so_a = 4u * ((uint32_t)p.off_i2h_w + 128u * r);
+        S.so_b = 4u * ((uint32_t)p.off_h2h_w + 128u * r);
+        S.bso = 4u * (bmin + r);
+        S.bda = 4u * (ib - bmin); S.bdb = 4u * (hb - bmin);
+        S.valid = 64;
+        return S;
+    };
+    const int b0 = nl & 1;                                       // next free stage buffer
+    stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
+    stage64_store(lds + b0 * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
+    __syncthreads();
+    f32x16 hold;
+    // fold of gate tile m (s_ = its gate sums) into the unit block's c' / h'
+    auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) {
+        const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
+        const int U = m / 5, j5 = m % 5;
+        if (j5 == 0) {                                           // g1
+            hold = s_;
+        } else if (j5 == 1) {                                    // g = max(g1, g2)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hold[r] = hold[r] > s_[r] ? hold[r] : s_[r];
+        } else if (j5 == 2) {                                    // ig * g
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hold[r] = CELL_SIG(s_[r]) * hold[r];
+        } else if (j5 == 3) {                                    // c' = f * c + ig * g
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float fcv = CELL_SIG(s_[r]) * cpre[r];
+                const float cn = fcv + hold[r];
+                st1(c.scr_r, lo_, C_SLOT(16 * U + r), cn);
+                hold[r] = cn;
+            }
+        } else {                                                 // h' = o * tanh(c')
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                st1(c.scr_r, lo_, H_SLOT(16 * U + r), CELL_SIG(s_[r]) * CELL_TANH(hold[r]));
+        }
+    };
+    auto load_c = [&](int m) {                                   // c of the f tile's unit block
+        f32x16 cp;
         const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
 #pragma unroll
-        for (int r = 0; r < 16; ++r) st1(c.scr_r, lo_, P_SLOT(16 * (5 * (ma / 5) + tile_q(ma)) + r), acc0[r]);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) st1(c.scr_r, lo_, P_SLOT(16 * (5 * (mb / 5) + tile_q(mb)) + r), acc1[r]);
-        if (more) stage64_store(lds + ((s + 1) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
+        for (int r = 0; r < 16; ++r) cp[r] = (m % 5 == 3 && t >= 0) ? ld1(c.scr_r, lo_, C_SLOT(16 * (m / 5) + r)) : 0.f;
+        return cp;
+    };
+#pragma unroll 1
+    for (int m = 0; m < 20; ++m) {
+        const f32x16 cpre = load_c(m);                           // before the staging loads (in-order vmcnt)
+        __builtin_amdgcn_sched_barrier(0);
+        if (m < 19) stage64_load(csrc(m + 1), c.wave * 64 + lane_fresh(), s64);
+        const float* buf = lds + ((m + b0) & 1) * STAGE64_FLOATS;
+        f32x16 a0, a1;
+        mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
+        fold(m, a0 + a1, cpre);                                  // i2h(x) + h2h(h), nets.py:109-111
+        if (m < 19) stage64_store(lds + ((m + 1 + b0) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
         __syncthreads();
     }
     PROF_MARK(2 * (t + 1) + 1);
@@ -721,24 +700,19 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
     const size_t lds32 = (size_t)(2 * STAGE_FLOATS) * sizeof(float);
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)nicnes_decode_stage_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds64);
-        if (e == hipSuccess) e = hipFuncSetAttribute((const void*)nicnes_decode_cell_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds64);
+        hipError_t e = hipFuncSetAttribute((const void*)nicnes_decode_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds64);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    if (evs && 2 * p->T + 5 > DECODE_MAX_EVENTS) return hipErrorInvalidValue;
+    if (evs && p->T + 4 > DECODE_MAX_EVENTS) return hipErrorInvalidValue;
     int ne = 0;
     auto mark = [&]() { if (evs) (void)hipEventRecord(evs[ne++], stream); };
     const dim3 grid(member_count, nslabs), block(NTHREADS);
     mark();
     hipLaunchKernelGGL(nicnes_decode_img_kernel, grid, block, lds32, stream, *p);
     mark();
-    hipLaunchKernelGGL(nicnes_decode_stage_kernel, grid, block, lds64, stream, *p, -1);
-    mark();
-    for (int t = 0; t <= p->T; ++t) {
-        hipLaunchKernelGGL(nicnes_decode_cell_kernel, grid, block, lds64, stream, *p, t);
-        mark();
-        hipLaunchKernelGGL(nicnes_decode_stage_kernel, grid, block, lds64, stream, *p, t);
+    for (int t = -1; t <= p->T; ++t) {
+        hipLaunchKernelGGL(nicnes_decode_step_kernel, grid, block, lds64, stream, *p, t);
         mark();
     }
     return hipGetLastError();

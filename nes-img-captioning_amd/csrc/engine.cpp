@@ -406,7 +406,7 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
     HIPC(h, hipMemsetAsync(p.seq, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(int32_t), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
     HIPC(h, nicnes_launch_decode(&p, count, nslabs_of(h->B), s, h->timing ? h->dev : nullptr));
-    h->n_dev = h->timing ? 2 * p.T + 5 : 0;
+    h->n_dev = h->timing ? p.T + 4 : 0;
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     CiderTables tb = tables_of(h);
     if (h->img_tables)
@@ -547,18 +547,19 @@ int nicnes_decode_phase_times(nicnes_handle* h, float* out4_host) {
     if (!h || !out4_host || h->n_dev < 5) return NICNES_ERR_INVALID;
     HIPC(h, hipSetDevice(h->device));
     HIPC(h, hipEventSynchronize(h->dev[h->n_dev - 1]));
-    // event k follows launch k: img, stage(-1), then cell(t), stage(t) for t = 0..T
-    float img = 0.f, cell = 0.f, stage = 0.f, ms = 0.f;
+    // event k follows launch k: img, then step(t) for t = -1..T. Steps -1 and 0 run only a cell
+    // (no logits); every later step runs logits + token, then the next cell.
+    float img = 0.f, cell_only = 0.f, step = 0.f, ms = 0.f;
     for (int k = 1; k < h->n_dev; ++k) {
         HIPC(h, hipEventElapsedTime(&ms, h->dev[k - 1], h->dev[k]));
         if (k == 1) img += ms;
-        else if (k % 2 == 0) stage += ms;
-        else cell += ms;
+        else step += ms;
+        if (k == 2 || k == 3) cell_only += ms;
     }
     out4_host[0] = img;
-    out4_host[1] = cell;
-    out4_host[2] = stage;
-    out4_host[3] = (float)(h->n_dev / 2);
+    out4_host[1] = cell_only;
+    out4_host[2] = step;
+    out4_host[3] = (float)(h->n_dev - 2);
     return NICNES_OK;
 }
 

@@ -228,12 +228,13 @@ class Engine:
         return float(out[0]), float(out[1])
 
     def decode_phase_times(self):
-        """Per-kernel split of the last timed decode: {'img_ms', 'cell_ms', 'stage_ms', 'stage_launches'}
-        (cell/stage summed over their T+1 / T+2 launches; HIP events between the launches)."""
+        """Per-kernel split of the last timed decode: {'img_ms', 'cell_only_ms', 'step_ms',
+        'step_launches'} (step_ms sums the T+2 step-kernel launches, cell_only_ms its two launches
+        without logits, t = -1 and 0; HIP events between the launches)."""
         out = (ctypes.c_float * 4)()
         check(self.L.nicnes_decode_phase_times(self.h, out), self.h, 'decode_phase_times')
-        return {'img_ms': float(out[0]), 'cell_ms': float(out[1]), 'stage_ms': float(out[2]),
-                'stage_launches': int(out[3])}
+        return {'img_ms': float(out[0]), 'cell_only_ms': float(out[1]), 'step_ms': float(out[2]),
+                'step_launches': int(out[3])}
 
     def stats(self):
         out = (ctypes.c_int64 * 4)()

@@ -19,8 +19,7 @@ def launch_spans(k, seq):
     """DECODE_PROF=1 build: per-launch span, workgroup durations, per-CU busy time, in-kernel clock."""
     raw = seq.reshape(-1, 4096).cpu().numpy().astype(np.int64) & 0xffffffff
     ts, cyc, hw = raw[:, :1024], raw[:, 1024:2048], raw[:, 2048:]
-    launches = [('img', 80)] + [('stage%d' % t, 2 * (t + 1)) for t in range(-1, 17)] + \
-               [('cell%d' % t, 40 + 2 * t) for t in range(0, 17)]
+    launches = [('img', 80)] + [('step%d' % t, 2 * (t + 1)) for t in range(-1, 17)]
     t0 = ts[:, 80].min()
     rows = []
     for name, sl in launches:
@@ -96,8 +95,8 @@ def main():
     base = np.median(res['base'])
     out = {k: {'median_ms': round(float(np.median(v)), 3), 'min_ms': round(float(np.min(v)), 3),
                'vs_base': round(float(np.median(v) / base), 3),
-               'stage_ms': round(float(np.median([ph['stage_ms'] for ph in phase[k]])), 3),
-               'cell_ms': round(float(np.median([ph['cell_ms'] for ph in phase[k]])), 3),
+               'step_ms': round(float(np.median([ph['step_ms'] for ph in phase[k]])), 3),
+               'cell_only_ms': round(float(np.median([ph['cell_only_ms'] for ph in phase[k]])), 3),
                'img_ms': round(float(np.median([ph['img_ms'] for ph in phase[k]])), 3),
                'tie_fallbacks': engines[k].stats()['tie_fallbacks']} for k, v in res.items()}
     print(json.dumps(out, indent=1))

@@ -7,7 +7,7 @@ Counter values are taken per dispatch of the kernel (dispatches whose name match
 is the largest seen for it -- the bench's sigma = 0 single-member setup evaluate is dropped --
 minus the first `--skip` ones) and averaged.
 
-usage: python scripts/pmc_traffic.py --fetch DIR --write DIR --kernel nicnes_decode_stage_kernel \
+usage: python scripts/pmc_traffic.py --fetch DIR --write DIR --kernel nicnes_decode_step_kernel \
            --algorithmic-bytes N --out profiles/r01_decode_pmc.json
 """
 import argparse
@@ -41,7 +41,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--fetch', required=True)
     ap.add_argument('--write', required=True)
-    ap.add_argument('--kernel', default='nicnes_decode_stage_kernel')
+    ap.add_argument('--kernel', default='nicnes_decode_step_kernel')
     ap.add_argument('--skip', type=int, default=0)
     ap.add_argument('--algorithmic-bytes', type=float, default=None)
     ap.add_argument('--out', required=True)

@@ -17,5 +17,5 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write_$TAG -o ru
 python scripts/trace_summary.py --trace gpurun_out/prof_stats_$TAG --command "python3 bench.py --steps 10 --warmup 2" \
     --out gpurun_out/decode_launches_$TAG.json > /dev/null
 python scripts/pmc_traffic.py --fetch gpurun_out/prof_fetch_$TAG --write gpurun_out/prof_write_$TAG \
-    --kernel nicnes_decode_stage_kernel --out gpurun_out/decode_pmc_$TAG.json > /dev/null
+    --kernel nicnes_decode_step_kernel --out gpurun_out/decode_pmc_$TAG.json > /dev/null
 echo done
