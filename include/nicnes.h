@@ -90,6 +90,22 @@ int nicnes_noise_indices(nicnes_handle* h, uint64_t iteration, int32_t member_be
 int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
                     double* fitness_out, int32_t* seq_out, void* stream);
 
+/* Fitness criterion (Fitness enum + get_criterium, src/captioning/policies.py:22-61, applied at
+ * :119-125): GREEDY = 100 * mean CIDEr-D; the greedy_* modes weight each step's probability of the
+ * greedy token by the row's CIDEr-D (src/captioning/fitness.py:43-132). Other modes (sample,
+ * self_critical, sc_loss) return NICNES_ERR_UNSUPPORTED. */
+#define NICNES_FITNESS_GREEDY 0
+#define NICNES_FITNESS_GREEDY_LOGPROB 1   /* AltLogFitnessCriterion */
+#define NICNES_FITNESS_GREEDY_EXPPROB 2   /* ExpFitnessCriterion */
+#define NICNES_FITNESS_GREEDY_LINPROB 3   /* LinFitnessCriterion */
+#define NICNES_FITNESS_GREEDY_AVGPROB 4   /* AvgLogFitnessCriterion */
+int nicnes_set_fitness_mode(nicnes_handle* h, int32_t mode);
+
+/* nicnes_evaluate plus the per-step log-prob of each greedy token, FCModel._sample's seq_logprobs
+ * (src/captioning/nets.py:191,208,241): logprob_out [count, 2, B, seq_length] fp32 or NULL. */
+int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
+                       double* fitness_out, int32_t* seq_out, float* logprob_out, void* stream);
+
 /* Centred ranks + antithetic weights over the WHOLE population, replaces
  * NESMaster.compute_centered_ranks and the weights line of gradient_estimate
  * (src/algorithm/nic_nes/nic_nes_master.py:170-205). fitness [P, 2] fp64 -> cr [P, 2] (or NULL),

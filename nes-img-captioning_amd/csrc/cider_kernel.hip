@@ -145,9 +145,57 @@ __global__ __launch_bounds__(256) void nicnes_cook_refs_kernel(const int32_t* re
     }
 }
 
+// ---- fitness of one candidate from its per-row CIDEr-D scores (whole workgroup) ----------------
+// crit 0 ('greedy'): float(cider * 100) (policies.py:125). crit 1-4 (greedy_logprob / expprob /
+// linprob / avgprob, picked by Fitness.get_criterium, policies.py:50-61): the criterion over the
+// per-step log-probs, rewards = per-row score as fp32 (policies.py:121,191), mask = 1 at t = 0 then
+// seq[t-1] > 0; elementwise in fp32 as torch does, sum(out) / sum(mask) accumulated in fp64
+// (fitness.py:43-132).
+__device__ void finish_fitness(const double* row_score, const int32_t* seq, const float* lp, int B, int T, int crit,
+                               double* out) {
+    if (crit == 0 || lp == nullptr) {
+        if (threadIdx.x == 0) {
+            double s = 0.0;
+            for (int b = 0; b < B; ++b) s += row_score[b];
+            *out = (s / (double)B) * 100.0;
+        }
+        return;
+    }
+    __shared__ double red_num[256], red_den[256];
+    double num = 0.0, den = 0.0;
+    const float third = (float)(1.0 / 9.0), l9 = (float)0.9542425094393249, em1 = (float)(2.718281828459045 - 1.0);
+    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+        const float reward = (float)row_score[b];
+        for (int t = 0; t < T; ++t) {
+            if (t > 0 && seq[(size_t)b * T + t - 1] <= 0) break;   // masked from here on
+            const float p = expf(lp[(size_t)b * T + t]);
+            float o;
+            if (crit == 2) {
+                o = (expf(p) - 1.0f) / em1 * reward;
+            } else if (crit == 3) {
+                o = p * reward;
+            } else {
+                const float pfact = log10f(p + third) + l9;
+                o = crit == 1 ? pfact * reward : 0.5f * reward + 0.5f * pfact * reward;
+            }
+            num += (double)o;
+            den += 1.0;
+        }
+    }
+    red_num[threadIdx.x] = num;
+    red_den[threadIdx.x] = den;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double sn = 0.0, sd = 0.0;
+        for (int i = 0; i < (int)blockDim.x; ++i) { sn += red_num[i]; sd += red_den[i]; }
+        *out = sn / sd;
+    }
+}
+
 // ---- candidates: one workgroup per candidate, one wave per image row ---------------------------
 __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, int B, int T, CiderTables tb,
-                                                           const int32_t* img_ref_start, double* fitness_out) {
+                                                           const int32_t* img_ref_start, const float* lp, int crit,
+                                                           double* fitness_out) {
     __shared__ double row_score[1024];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int cand = blockIdx.x;
@@ -187,11 +235,8 @@ __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, i
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double s = 0.0;
-        for (int b = 0; b < B; ++b) s += row_score[b];
-        fitness_out[cand] = (s / (double)B) * 100.0;        // float(cider * 100), policies.py:125
-    }
+    finish_fitness(row_score, seq + (size_t)cand * B * T, lp ? lp + (size_t)cand * B * T : nullptr, B, T, crit,
+                   fitness_out + cand);
 }
 
 extern "C" uint64_t nicnes_df_hash_capacity(int64_t n) {
@@ -216,9 +261,11 @@ extern "C" hipError_t nicnes_launch_cook_refs(const int32_t* ref_tokens, int n_r
 }
 
 extern "C" hipError_t nicnes_launch_cider(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
-                                          const int32_t* img_ref_start, double* fitness_out, hipStream_t stream) {
+                                          const int32_t* img_ref_start, const float* lp, int crit,
+                                          double* fitness_out, hipStream_t stream) {
     if (B > 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(nicnes_cider_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, *tb, img_ref_start, fitness_out);
+    hipLaunchKernelGGL(nicnes_cider_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, *tb, img_ref_start, lp, crit,
+                       fitness_out);
     return hipGetLastError();
 }
 
@@ -265,7 +312,8 @@ __global__ __launch_bounds__(64) void nicnes_img_ngram_kernel(const int32_t* img
 // candidates scored against the image table: one probe per distinct n-gram, then the per-reference
 // weights are consecutive doubles (same arithmetic and order as nicnes_cider_kernel)
 __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* seq, int B, int T, CiderTables tb,
-                                                               const int32_t* img_ref_start, double* fitness_out) {
+                                                               const int32_t* img_ref_start, const float* lp,
+                                                               int crit, double* fitness_out) {
     __shared__ double row_score[1024];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int cand = blockIdx.x;
@@ -309,11 +357,8 @@ __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* se
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        double s = 0.0;
-        for (int b = 0; b < B; ++b) s += row_score[b];
-        fitness_out[cand] = (s / (double)B) * 100.0;        // float(cider * 100), policies.py:125
-    }
+    finish_fitness(row_score, seq + (size_t)cand * B * T, lp ? lp + (size_t)cand * B * T : nullptr, B, T, crit,
+                   fitness_out + cand);
 }
 
 extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int B, const CiderTables* tb,
@@ -323,9 +368,10 @@ extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int
 }
 
 extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
-                                              const int32_t* img_ref_start, double* fitness_out, hipStream_t stream) {
+                                              const int32_t* img_ref_start, const float* lp, int crit,
+                                              double* fitness_out, hipStream_t stream) {
     if (B > 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(nicnes_cider_img_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, *tb, img_ref_start,
-                       fitness_out);
+    hipLaunchKernelGGL(nicnes_cider_img_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, *tb, img_ref_start, lp,
+                       crit, fitness_out);
     return hipGetLastError();
 }

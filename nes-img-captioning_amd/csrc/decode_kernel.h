@@ -10,6 +10,7 @@ struct DecodeParams {
     const uint64_t* noise_idx;   // per member slice start (multiple of 64)
     const float* fc;             // unique-image fc features [B, F]
     int32_t* seq;                // out: [members, 2, B, T] greedy tokens (masked after the first 0)
+    float* lp;                   // out (nullable): [members, 2, B, T] log-prob of the greedy token (nets.py:208,241)
     float* scratch;              // nicnes_decode_scratch_floats(): lane-private c | h' | x0 | unfinished
     int32_t* stats;              // [0] = exact-pass fallbacks (atomic)
     int32_t* alive;              // [members * slabs]: 0 once every row of the workgroup finished

@@ -600,7 +600,12 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         it = unfinished ? tok : 0;
         st1(c.scr_r, lo, U_SLOT, unfinished ? 1.f : 0.f);
 #if !DECODE_PROF
-        if (c.hh == 0 && c.row_valid) p.seq[(((size_t)c.member * 2 + c.sgn) * p.B + c.b) * p.T + (t - 1)] = it;
+        if (c.hh == 0 && c.row_valid) {
+            const size_t o = (((size_t)c.member * 2 + c.sgn) * p.B + c.b) * p.T + (t - 1);
+            p.seq[o] = it;
+            // seq_logprobs[:, t-1] = max lp = fp32((m - m) - lse) = -lse (nets.py:208,241)
+            if (p.lp) p.lp[o] = -lse;
+        }
 #endif
         const int any = __syncthreads_or(((unfinished && c.row_valid) || (DECODE_ABLATE & 64)) ? 1 : 0);
         if (c.tid == 0) p.alive[c.wg] = any;

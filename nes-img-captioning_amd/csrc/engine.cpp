@@ -64,6 +64,8 @@ struct nicnes_handle {
 
     uint64_t* nidx = nullptr;
     int32_t* seq = nullptr;
+    float* lp = nullptr;              // per-step log-probs for the greedy_* criteria
+    int fitness_mode = 0;             // nicnes_set_fitness_mode (0 = 'greedy')
     float* dscratch = nullptr;
     int32_t* stats = nullptr;
     int32_t* alive = nullptr;         // per decode workgroup: rows left unfinished
@@ -184,6 +186,7 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
     if (!rc) rc = dalloc(h, &h->img_vr, MB * IMG_ROWS * IMG_MAXR);
     if (!rc) rc = dalloc(h, &h->nidx, MM);
     if (!rc) rc = dalloc(h, &h->seq, MM * 2 * MB * T);
+    if (!rc) rc = dalloc(h, &h->lp, MM * 2 * MB * T);
     {
         const char* fe = getenv("NICNES_FORCE_EXACT");
         h->force_exact = (fe && fe[0] == '1') ? 1 : 0;
@@ -212,7 +215,7 @@ int nicnes_destroy(nicnes_handle* h) {
     if (!h) return NICNES_OK;
     (void)hipSetDevice(h->device);
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
-                    h->ref_norm, h->nidx, h->seq, h->dscratch, h->stats, h->partials, h->norms,
+                    h->ref_norm, h->nidx, h->seq, h->lp, h->dscratch, h->stats, h->partials, h->norms,
                     h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -366,8 +369,21 @@ int nicnes_noise_indices(nicnes_handle* h, uint64_t iteration, int32_t member_be
     return NICNES_OK;
 }
 
+int nicnes_set_fitness_mode(nicnes_handle* h, int32_t mode) {
+    if (!h) return NICNES_ERR_INVALID;
+    if (mode < NICNES_FITNESS_GREEDY || mode > NICNES_FITNESS_GREEDY_AVGPROB)
+        return fail(h, NICNES_ERR_UNSUPPORTED, "fitness mode: the engine implements greedy and greedy_{log,exp,lin,avg}prob");
+    h->fitness_mode = mode;
+    return NICNES_OK;
+}
+
 int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
                     double* fitness_out, int32_t* seq_out, void* stream) {
+    return nicnes_evaluate_lp(h, iteration, member_begin, count, sigma, fitness_out, seq_out, nullptr, stream);
+}
+
+int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
+                       double* fitness_out, int32_t* seq_out, float* logprob_out, void* stream) {
     if (!h || !fitness_out || member_begin < 0) return NICNES_ERR_INVALID;
     if (count < 1 || count > h->cfg.max_members) return fail(h, NICNES_ERR_INVALID, "count out of [1, max_members]");
     if (!h->noise) return fail(h, NICNES_ERR_INVALID, "nicnes_set_noise_table first");
@@ -383,6 +399,7 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
     p.noise_idx = h->nidx;
     p.fc = h->fc;
     p.seq = seq_out ? seq_out : h->seq;
+    p.lp = logprob_out ? logprob_out : (h->fitness_mode ? h->lp : nullptr);
     p.scratch = h->dscratch;
     p.stats = h->stats;
     p.alive = h->alive;
@@ -404,15 +421,18 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
     p.off_h2h_b = h->off[8];
     // rows a member never writes (all finished early) must read as 0 (nets.py:188 zeros)
     HIPC(h, hipMemsetAsync(p.seq, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(int32_t), s));
+    if (p.lp) HIPC(h, hipMemsetAsync(p.lp, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(float), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
     HIPC(h, nicnes_launch_decode(&p, count, nslabs_of(h->B), s, h->timing ? h->dev : nullptr));
     h->n_dev = h->timing ? p.T + 4 : 0;
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     CiderTables tb = tables_of(h);
     if (h->img_tables)
-        HIPC(h, nicnes_launch_cider_img(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, fitness_out, s));
+        HIPC(h, nicnes_launch_cider_img(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, p.lp,
+                                         h->fitness_mode, fitness_out, s));
     else
-        HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, fitness_out, s));
+        HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, p.lp,
+                                         h->fitness_mode, fitness_out, s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[2], s));
     return NICNES_OK;
 }

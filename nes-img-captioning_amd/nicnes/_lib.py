@@ -15,7 +15,7 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_get_adam_state', 'nicnes_set_batch', 'nicnes_set_df_table', 'nicnes_noise_indices',
            'nicnes_evaluate', 'nicnes_rank_weights', 'nicnes_grad_partial', 'nicnes_adam_step', 'nicnes_stats',
            'nicnes_set_timing', 'nicnes_kernel_times', 'nicnes_decode_phase_times', 'nicnes_sgd_step',
-           'nicnes_optimizer_update', 'nicnes_last_ratio']
+           'nicnes_optimizer_update', 'nicnes_last_ratio', 'nicnes_set_fitness_mode', 'nicnes_evaluate_lp']
 
 
 class NicnesConfig(ctypes.Structure):
@@ -59,6 +59,8 @@ def lib(path=None):
         'nicnes_set_df_table': (c.c_int, [vp, vp, vp, i64, f64]),
         'nicnes_noise_indices': (c.c_int, [vp, u64, i32, i32, vp, vp]),
         'nicnes_evaluate': (c.c_int, [vp, u64, i32, i32, f32, vp, vp, vp]),
+        'nicnes_evaluate_lp': (c.c_int, [vp, u64, i32, i32, f32, vp, vp, vp, vp]),
+        'nicnes_set_fitness_mode': (c.c_int, [vp, i32]),
         'nicnes_rank_weights': (c.c_int, [vp, vp, i32, vp, vp, vp]),
         'nicnes_grad_partial': (c.c_int, [vp, u64, i32, i32, vp, f32, vp, vp]),
         'nicnes_adam_step': (c.c_int, [vp, vp, i32, f64, f64, f64, f64, f64, vp, vp]),

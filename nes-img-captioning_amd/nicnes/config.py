@@ -6,7 +6,8 @@ Field names and defaults mirror
   ModelOptions      /root/reference/src/algorithm/policies.py:36-41
   optimizer_options /root/reference/src/algorithm/nic_nes/experiment.py:20-21
 A leading underscore disables a key ("_from_infos"), as in the reference JSON files. The engine
-implements the mscoco_nes.json hot path only: net 'fc_caption', fitness 'greedy', no vbn /
+implements the mscoco_nes.json hot path only: net 'fc_caption', fitness 'greedy' or one of the
+greedy_* criteria (greedy_logprob / expprob / linprob / avgprob), no vbn /
 layer_n / safe mutations; anything else raises NotSupported (nicnes_create returns
 NICNES_ERR_UNSUPPORTED for unsupported model sizes).
 """
@@ -31,6 +32,11 @@ _model_opt_fields = ['vocab_size', 'input_encoding_size', 'rnn_type', 'rnn_size'
                      'layer_n_affine', 'safe_mutation_underflow', 'safe_mutations', 'safe_mutation_vector',
                      'safe_mutation_batch_size']
 ModelOptions = namedtuple('ModelOptions', field_names=_model_opt_fields, defaults=(0,) * len(_model_opt_fields))
+
+
+# Fitness modes the engine implements: greedy decoding, scored by CIDEr-D alone or by a criterion
+# over the greedy tokens' log-probs (Fitness.is_greedy, src/captioning/policies.py:45-47)
+GREEDY_FITNESS = ('greedy', 'greedy_logprob', 'greedy_expprob', 'greedy_linprob', 'greedy_avgprob')
 
 
 class NotSupported(ValueError):
@@ -75,14 +81,20 @@ class ExperimentSpec:
         po, mo = self.policy_options, self.model_options
         if po.net != 'fc_caption':
             raise NotSupported('net %r: the engine implements fc_caption' % po.net)
-        if (po.fitness or 'greedy') != 'greedy':
-            raise NotSupported("fitness %r: the engine implements 'greedy' (100 * mean CIDEr-D)" % po.fitness)
+        if self.fitness not in GREEDY_FITNESS:
+            raise NotSupported("fitness %r: the engine implements %s (src/captioning/policies.py:22-61)"
+                               % (po.fitness, ', '.join(GREEDY_FITNESS)))
         if po.vbn or mo.vbn_e or mo.layer_n:
             raise NotSupported('virtual batch norm / layer norm are not implemented by the engine')
         if (po.safe_mutations or '') or (mo.safe_mutations or ''):
             raise NotSupported('safe mutations are not implemented by the engine')
 
     # ------------------------------------------------------------------------------------
+    @property
+    def fitness(self):
+        """policy_options.fitness; Fitness.DEFAULT is 'greedy' (policies.py:35)."""
+        return self.policy_options.fitness or 'greedy'
+
     @property
     def sigma(self):
         return float(self.config.noise_stdev)

@@ -154,17 +154,33 @@ class Engine:
                                               self._stream()), self.h, 'noise_indices')
         return out
 
-    def evaluate(self, iteration, member_begin, count, sigma, fitness_out=None, return_seq=False):
-        """Fitness (f+, f-) of members [member_begin, +count): tensor [count, 2] fp64 on the GPU."""
+    # Fitness enum values the engine implements (src/captioning/policies.py:22-35) -> nicnes.h codes
+    FITNESS_MODES = {'greedy': 0, 'greedy_logprob': 1, 'greedy_expprob': 2, 'greedy_linprob': 3,
+                     'greedy_avgprob': 4}
+
+    def set_fitness_mode(self, fitness):
+        """Fitness criterion by its experiment-JSON name (policy_options.fitness) or nicnes.h code."""
+        code = self.FITNESS_MODES.get(fitness, fitness) if isinstance(fitness, str) else int(fitness)
+        if isinstance(code, str):
+            code = -1
+        check(self.L.nicnes_set_fitness_mode(self.h, code), self.h, 'set_fitness_mode(%r)' % (fitness,))
+        self.fitness_mode = code
+
+    def evaluate(self, iteration, member_begin, count, sigma, fitness_out=None, return_seq=False, return_lp=False):
+        """Fitness (f+, f-) of members [member_begin, +count): tensor [count, 2] fp64 on the GPU.
+        return_seq / return_lp add the greedy tokens [count, 2, B, T] int32 and their per-step
+        log-probs (FCModel._sample's seq_logprobs) [count, 2, B, T] fp32."""
         fit = fitness_out if fitness_out is not None else torch.empty((count, 2), dtype=torch.float64,
                                                                       device=self.device)
-        seq = torch.empty((count, 2, self.B, self.cfg.seq_length), dtype=torch.int32,
-                          device=self.device) if return_seq else None
+        shape = (count, 2, self.B, self.cfg.seq_length)
+        seq = torch.empty(shape, dtype=torch.int32, device=self.device) if return_seq else None
+        lp = torch.empty(shape, dtype=torch.float32, device=self.device) if return_lp else None
         with torch.cuda.device(self.device):
-            check(self.L.nicnes_evaluate(self.h, ctypes.c_uint64(iteration), member_begin, count,
-                                         ctypes.c_float(sigma), _ptr(fit), _ptr(seq), self._stream()), self.h,
-                  'evaluate')
-        return (fit, seq) if return_seq else fit
+            check(self.L.nicnes_evaluate_lp(self.h, ctypes.c_uint64(iteration), member_begin, count,
+                                            ctypes.c_float(sigma), _ptr(fit), _ptr(seq), _ptr(lp), self._stream()),
+                  self.h, 'evaluate')
+        out = (fit,) + ((seq,) if return_seq else ()) + ((lp,) if return_lp else ())
+        return out if len(out) > 1 else fit
 
     def rank_weights(self, fitness_all):
         """fitness [P, 2] fp64 (whole population) -> (centred ranks [P, 2] fp64, weights [P] fp32)."""

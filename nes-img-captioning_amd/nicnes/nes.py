@@ -86,6 +86,8 @@ class EnginePolicy:
         self.spec = spec
         self.shapes = param_shapes(engine)
         self._batch_key = None
+        if spec is not None:
+            engine.set_fitness_mode(spec.fitness)      # CaptPolicy's Fitness (policies.py:22-61)
 
     # Policy.set_model (policies.py:125-147): PolicyNet-like object, state_dict, or .pth path
     def set_model(self, model):
@@ -130,7 +132,8 @@ class EnginePolicy:
         return fc.shape[0]
 
     def rollout(self, placeholder, data, config):
-        """CaptPolicy.rollout for fitness 'greedy': float(100 * mean CIDEr-D) of the current theta."""
+        """CaptPolicy.rollout (policies.py:86-128) of the current theta: float(100 * mean CIDEr-D) for
+        'greedy', the criterion value for the greedy_* fitness modes."""
         self._ensure_batch(data)
         fit = self.e.evaluate(0, 0, 1, 0.0)
         return float(fit[0, 0].item())

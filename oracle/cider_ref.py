@@ -123,6 +123,37 @@ def rollout_fitness(scorer, seq, gts_rows, seq_per_img=1):
     return float(score * 100), scores
 
 
+# greedy_* fitness criteria (pinned by tests/golden/fitness_criteria.npz, made from the reference's own
+# classes by scripts/make_golden.py). Codes match nicnes_set_fitness_mode.
+CRITERIA = {'greedy': 0, 'greedy_logprob': 1, 'greedy_expprob': 2, 'greedy_linprob': 3, 'greedy_avgprob': 4}
+
+
+def criterion_fitness(mode, lp, seq, scores):
+    """``crit(sample_logprobs, gen_result, rewards)`` of CaptPolicy.rollout (policies.py:119-123) for
+    the criteria Fitness.get_criterium picks (policies.py:50-61): AltLog (fitness.py:43-64), Exp
+    (:90-109), Lin (:112-132), AvgLog (:67-86). Elementwise in fp32 like torch; the sums in fp64.
+    ``lp`` f32 [N, T] per-step log-prob of the chosen token, ``seq`` [N, T], ``scores`` [N] CIDEr-D
+    per row (rewards = scores repeated over T, policies.py:191; cast to fp32 at policies.py:121)."""
+    code = CRITERIA[mode] if isinstance(mode, str) else int(mode)
+    lp = np.asarray(lp, np.float32)
+    N, T = lp.shape
+    reward = np.repeat(np.asarray(scores, np.float64).astype(np.float32)[:, None], T, 1)
+    mask = np.concatenate([np.ones((N, 1), np.float32), (np.asarray(seq)[:, :-1] > 0).astype(np.float32)], 1)
+    p = np.exp(lp)
+    pfact = np.log10(p + np.float32(1 / 9)) + np.float32(np.log10(9))
+    if code == 1:
+        out = pfact * reward * mask
+    elif code == 2:
+        out = (np.exp(p) - np.float32(1)) / np.float32(math.e - 1) * reward * mask
+    elif code == 3:
+        out = p * reward * mask
+    elif code == 4:
+        out = np.float32(0.5) * reward * mask + np.float32(0.5) * pfact * reward * mask
+    else:
+        raise ValueError('criterion %r' % (mode,))
+    return float(out.astype(np.float64).sum() / mask.astype(np.float64).sum())
+
+
 def document_frequency_from_refs(ref_sets):
     """df as self-critical's prepro_ngrams builds it: for every image (a set of ref strings),
     each distinct n-gram over its refs counts once. Returns (dict, ref_len_raw=len(ref_sets))."""

@@ -18,6 +18,10 @@ Fixtures (all .npz, loadable with allow_pickle=False):
   sgd.npz                         SGD.update (optimizers.py:38-47) driven like run_master, 3 steps
   adam_globalg64.npz              Adam.update(globalg) called directly with an fp64 globalg from the
                                   first step (the fp64 (1 - b) * g' branch while theta is still fp32)
+  fitness_criteria.npz            the greedy_* fitness criteria (src/captioning/fitness.py:43-132, chosen
+                                  by Fitness.get_criterium, src/captioning/policies.py:50-61) on seeded
+                                  logprobs / sequences / per-row CIDEr rewards, as CaptPolicy.rollout
+                                  calls them (policies.py:119-123)
 Pass fixture names to regenerate a subset: python scripts/make_golden.py sgd adam_globalg64
 """
 import json
@@ -199,6 +203,30 @@ def ranks_fixture():
     np.savez_compressed(os.path.join(OUT, 'ranks.npz'), x=x, y=y)
 
 
+def fitness_criteria_fixture():
+    import captioning.fitness as ref_fit  # noqa: E402  (reference module)
+    crits = {'greedy_logprob': ref_fit.AltLogFitnessCriterion, 'greedy_expprob': ref_fit.ExpFitnessCriterion,
+             'greedy_linprob': ref_fit.LinFitnessCriterion, 'greedy_avgprob': ref_fit.AvgLogFitnessCriterion}
+    rng = np.random.Generator(np.random.PCG64(77))
+    cases = {}
+    for case, (N, T) in enumerate([(8, 16), (40, 16), (5, 16)]):
+        seq = rng.integers(1, 50, (N, T)).astype(np.int64)
+        for i in range(N):                      # rows end at a random step (some never, one at t = 0)
+            end = 0 if i == 0 else int(rng.integers(1, T + 4))
+            if end < T:
+                seq[i, end:] = 0
+        lp = (-rng.exponential(1.5, (N, T))).astype(np.float32)
+        scores = rng.uniform(0, 3, N).astype(np.float64)
+        if case == 2:
+            scores[:] = 0.0
+        cases['seq_%d' % case], cases['lp_%d' % case], cases['scores_%d' % case] = seq, lp, scores
+        reward = np.repeat(scores[:, None], T, 1)          # compute_ciders, policies.py:191
+        for name, cls in crits.items():
+            out = cls()(torch.from_numpy(lp), torch.from_numpy(seq), torch.from_numpy(reward).float())
+            cases['%s_%d' % (name, case)] = np.array(float(out.item()))
+    np.savez_compressed(os.path.join(OUT, 'fitness_criteria.npz'), **cases)
+
+
 def all_fixtures():
     tiny = O.Dims(vocab_size=63, E=32, R=32, F=64)
     full = O.Dims()
@@ -211,6 +239,7 @@ def all_fixtures():
     ranks_fixture()
     sgd_fixture()
     adam_globalg64_fixture()
+    fitness_criteria_fixture()
 
 
 if __name__ == '__main__':

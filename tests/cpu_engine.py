@@ -24,6 +24,10 @@ class OracleEngine:
         self.adam = None
         self.theta32 = theta32.copy()
         self.theta_src = theta32.copy()
+        self.fitness_mode = 0
+
+    def set_fitness_mode(self, fitness):
+        self.fitness_mode = CR.CRITERIA[fitness] if isinstance(fitness, str) else int(fitness)
 
     # ---- Engine surface used by nicnes.nes / nicnes.master
     def set_theta(self, theta, fp32_origin=None):
@@ -65,8 +69,9 @@ class OracleEngine:
         for k in range(count):
             idx = self._idx(iteration, member_begin + k)
             for s, sign in enumerate((+1, -1)):
-                seq, _, _ = O.decode(self.dims, O.perturb(self.theta32, self.table, idx, sigma, sign), self.fc)
-                out[k, s] = CR.rollout_fitness(self.scorer, seq, self.gts)[0]
+                seq, lp, _ = O.decode(self.dims, O.perturb(self.theta32, self.table, idx, sigma, sign), self.fc)
+                f, scores = CR.rollout_fitness(self.scorer, seq, self.gts)
+                out[k, s] = CR.criterion_fitness(self.fitness_mode, lp, seq, scores) if self.fitness_mode else f
         return out
 
     def rank_weights(self, fitness_all):

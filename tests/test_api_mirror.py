@@ -11,6 +11,8 @@ from nicnes import config as C
 from nicnes import master as M
 from nicnes import nes as N
 from nicnes import transport as T
+from oracle import cider_ref as CR
+from oracle import oracle as O
 from tests.cpu_engine import OracleEngine, tiny_workload
 
 # the keys of /root/reference/experiments/mscoco_nes.json (values as in that file)
@@ -64,6 +66,14 @@ def test_spec_reads_mscoco_nes():
 def test_spec_rejects_unsupported(over):
     with pytest.raises(C.NotSupported):
         C.ExperimentSpec(_exp(**over))
+
+
+@pytest.mark.parametrize('fitness', ['greedy', 'greedy_logprob', 'greedy_expprob', 'greedy_linprob',
+                                     'greedy_avgprob', None])
+def test_spec_accepts_greedy_fitness_modes(fitness):
+    """Fitness.is_greedy modes (src/captioning/policies.py:45-47); None -> Fitness.DEFAULT 'greedy'."""
+    s = C.ExperimentSpec(_exp(policy_options={'net': 'fc_caption', 'fitness': fitness}))
+    assert s.fitness == (fitness or 'greedy')
 
 
 # ------------------------------------------------------------------ codec / store ------------------
@@ -176,9 +186,10 @@ def test_optimizer_file_reads_reference_layout(tmp_path):
 
 
 # ------------------------------------------------------------------ master loops ---------------------
-def _spec(P, opt='adam'):
+def _spec(P, opt='adam', fitness='greedy'):
     return C.ExperimentSpec(_exp(nb_offspring=P, config={'noise_stdev': 0.05, 'batch_size': 4, 'l2coeff': 1e-3,
                                                          'snapshot_freq': 1},
+                                 policy_options={'net': 'fc_caption', 'fitness': fitness},
                                  optimizer_options={'type': opt, 'args': {'stepsize': 0.01}}), vocab_size=63)
 
 
@@ -207,6 +218,21 @@ def test_dispatched_loop_matches_local_loop(workload, tmp_path, opt):
     assert np.array_equal(a64.numpy(), b64.numpy())
     assert [r['score_mean'] for r in local.stats] == [r['score_mean'] for r in master.stats]
     assert local.opt.t == iters == master.opt.t
+
+
+def test_worker_fitness_follows_spec_criterion(workload):
+    """EngineWorker built from a greedy_linprob spec scores members with the criterion
+    (CaptPolicy.rollout, policies.py:119-123), not with 100 * CIDEr."""
+    dims, theta, fc, gts, df, n, table = workload
+    batch = {'fc_feats': fc, 'gts': gts}
+    task = N.NESTask(current=None, batch_data=batch, noise_stdev=0.05, batch_size=4, iteration=1)
+    e = _engine(workload)
+    res = N.EngineWorker(e, _spec(2, 'adam', 'greedy_linprob'), worker_id=1).fitness_batch(0, task, 0, 2)
+    assert e.fitness_mode == 3
+    idx = O.noise_index(0, 1, 1, table.size, dims.D)
+    seq, lp, _ = O.decode(dims, O.perturb(theta, table, idx, 0.05, -1), fc)
+    _, scores = CR.rollout_fitness(e.scorer, seq, gts)
+    assert res[1].fitness[1] == CR.criterion_fitness('greedy_linprob', lp, seq, scores)
 
 
 def test_snapshot_roundtrip(workload, tmp_path):

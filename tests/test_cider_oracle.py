@@ -2,11 +2,14 @@
 the unvendored `cider` submodule, so these pin the restatement by hand-derived values
 (parity with the reference implementation itself: unpinned)."""
 import math
+import os
 
 import numpy as np
 import pytest
 
 from oracle import cider_ref as CR
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
 
 def test_array_to_str_includes_first_zero():
@@ -72,3 +75,27 @@ def test_rollout_fitness_dedup_equals_duplicated():
     f_unique, _ = CR.rollout_fitness(s, seq, gts, 1)
     f_dup, _ = CR.rollout_fitness(s, np.repeat(seq, 5, axis=0), gts, 5)
     assert f_unique == pytest.approx(f_dup, rel=1e-12)
+
+
+@pytest.mark.parametrize('mode', ['greedy_logprob', 'greedy_expprob', 'greedy_linprob', 'greedy_avgprob'])
+def test_criterion_oracle_matches_reference_golden(mode):
+    """greedy_* criteria (src/captioning/fitness.py:43-132) against the reference's own classes
+    (tests/golden/fitness_criteria.npz, scripts/make_golden.py); the reference sums in fp32."""
+    z = np.load(os.path.join(GOLDEN, 'fitness_criteria.npz'))
+    for c in range(3):
+        got = CR.criterion_fitness(mode, z['lp_%d' % c], z['seq_%d' % c], z['scores_%d' % c])
+        ref = float(z['%s_%d' % (mode, c)])
+        assert abs(got - ref) <= 1e-6 * max(1.0, abs(ref)), (c, got, ref)
+
+
+def test_criterion_duplicate_rows_invariant():
+    """The engine scores unique images once; the reference decodes each 5x (dataloader.py:175).
+    The criterion is a ratio of sums, so 5 identical copies give the same value."""
+    rng = np.random.Generator(np.random.PCG64(5))
+    seq = rng.integers(0, 9, (6, 16))
+    lp = -rng.exponential(1.0, (6, 16)).astype(np.float32)
+    sc = rng.uniform(0, 2, 6)
+    for mode in ('greedy_logprob', 'greedy_expprob', 'greedy_linprob', 'greedy_avgprob'):
+        a = CR.criterion_fitness(mode, lp, seq, sc)
+        b = CR.criterion_fitness(mode, np.repeat(lp, 5, 0), np.repeat(seq, 5, 0), np.repeat(sc, 5))
+        assert abs(a - b) <= 1e-12 * max(1.0, abs(a))

@@ -112,6 +112,74 @@ def test_cider_fitness_matches_oracle(eng, n_refs):
     assert fit.max() > 0.0
 
 
+def _mask(seq):
+    """positions the criteria count: t = 0, then seq[t-1] > 0 (src/captioning/fitness.py:57-58)"""
+    return np.concatenate([np.ones((seq.shape[0], 1), bool), seq[:, :-1] > 0], 1)
+
+
+def test_logprobs_match_oracle(eng):
+    """seq_logprobs (nets.py:208,241): the greedy token's log-prob, -lse of the step, on every
+    position a criterion counts; 1e-5 absolute (lse summed in another order than the oracle's)."""
+    dims = O.Dims()
+    theta = O.make_theta(dims, 0, 4.0, 0.1)
+    fc = np.random.Generator(np.random.PCG64(4321)).standard_normal((36, dims.F)).astype(np.float32)
+    _load(eng, theta, fc)
+    _, seq, lp = eng.evaluate(3, 0, 2, SIGMA, return_seq=True, return_lp=True)
+    seq, lp = seq.cpu().numpy(), lp.cpu().numpy()
+    idx = eng.noise_indices(3, 0, 2).cpu().numpy()
+    for k in range(2):
+        for s, sign in enumerate((+1, -1)):
+            oseq, olp, fr = O.decode(dims, O.perturb(theta, eng._table_np, int(idx[k]), SIGMA, sign), fc)
+            assert np.array_equal(seq[k, s], oseq)
+            m = _mask(oseq)
+            assert np.abs(lp[k, s][m] - olp[m]).max() <= 1e-5
+            assert (lp[k, s][m] <= 0).all() and np.isfinite(lp[k, s]).all()
+
+
+@pytest.mark.parametrize('n_refs', [5, 10], ids=['image_tables', 'scan_over_8_refs'])
+@pytest.mark.parametrize('mode', ['greedy_logprob', 'greedy_expprob', 'greedy_linprob', 'greedy_avgprob'])
+def test_fitness_criteria_match_oracle(eng, mode, n_refs):
+    """greedy_* fitness (policies.py:50-61,119-123; fitness.py:43-132) on the GPU against the oracle
+    criterion (pinned by tests/golden/fitness_criteria.npz): 1e-6 relative on the GPU's own log-probs,
+    1e-5 relative end to end against the oracle's decode."""
+    import nicnes.synthetic as S
+    dims = O.Dims()
+    theta = O.make_theta(dims, 0, 4.0, 0.1)
+    B = 24
+    fc = np.random.Generator(np.random.PCG64(1234)).standard_normal((B, dims.F)).astype(np.float32)
+    base, _, _ = O.decode(dims, theta, fc)
+    gts, df, ref_len_raw = S.build_references(base, dims.vocab_size, seed=11, n_refs=n_refs, df_sets=256)
+    _load(eng, theta, fc, gts, df, ref_len_raw)
+    eng.set_fitness_mode(mode)
+    try:
+        fit, seq, lp = eng.evaluate(2, 0, 2, SIGMA, return_seq=True, return_lp=True)
+        fit_nolp = eng.evaluate(2, 0, 2, SIGMA).cpu().numpy()
+    finally:
+        eng.set_fitness_mode('greedy')
+    fit, seq, lp = fit.cpu().numpy(), seq.cpu().numpy(), lp.cpu().numpy()
+    assert np.array_equal(fit, fit_nolp)                  # internal log-prob buffer == caller's
+    scorer = CR.CiderDOracle(df, ref_len_raw)
+    idx = eng.noise_indices(2, 0, 2).cpu().numpy()
+    for k in range(2):
+        for s, sign in enumerate((+1, -1)):
+            _, scores = CR.rollout_fitness(scorer, seq[k, s], gts)
+            f_own = CR.criterion_fitness(mode, lp[k, s], seq[k, s], scores)
+            assert abs(fit[k, s] - f_own) <= 1e-6 * max(1.0, abs(f_own)), (k, s, fit[k, s], f_own)
+            oseq, olp, _ = O.decode(dims, O.perturb(theta, eng._table_np, int(idx[k]), SIGMA, sign), fc)
+            assert np.array_equal(seq[k, s], oseq)
+            f_ora = CR.criterion_fitness(mode, olp, oseq, scores)
+            assert abs(fit[k, s] - f_ora) <= 1e-5 * max(1.0, abs(f_ora)), (k, s, fit[k, s], f_ora)
+    assert fit.max() > 0.0
+
+
+def test_fitness_mode_rejects_unsupported(eng):
+    import nicnes
+    for bad in ('sample', 'self_critical', 'sc_loss', 7):
+        with pytest.raises((nicnes.NicnesError, ValueError, RuntimeError)):
+            eng.set_fitness_mode(bad)
+    eng.set_fitness_mode('greedy')
+
+
 def test_rank_weights_bit_exact(eng):
     rng = np.random.default_rng(5)
     fit = np.round(rng.random((300, 2)) * 20) / 2.0        # many ties
