@@ -79,6 +79,8 @@ def main():
     ap.add_argument('--sigma', type=float, default=0.01)
     ap.add_argument('--noise-len', type=int, default=1 << 27)
     ap.add_argument('--bu', action='store_true', help="'bu' features: ReLU(N(0,1)) fc (configs[4])")
+    ap.add_argument('--fitness', default='greedy', help="policy_options.fitness: greedy (mscoco_nes.json) or "
+                    "greedy_logprob / greedy_expprob / greedy_linprob / greedy_avgprob")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-cores', type=int, default=16)
     ap.add_argument('--cpu-members-per-core', type=int, default=1)
@@ -109,6 +111,7 @@ def main():
     eng = nicnes.Engine(max_batch=B, max_members=P_local, noise_len=args.noise_len, noise_seed=0,
                         device=local_rank)
     S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu)
+    eng.set_fitness_mode(args.fitness)
     runner = PopulationRunner(eng, P, args.sigma, l2coeff=1e-7, stepsize=1e-3, rank=rank, world_size=world,
                               group=group)
     it = 1
@@ -160,7 +163,8 @@ def main():
         'data': 'synthetic (seeded fc features, xavier-init fc_caption theta, substituted refs, 2^27 noise table)',
         'config': {'workload': 'mscoco_nes.json fc_caption, pop=%d antithetic (%d/GPU), batch_size=%d unique '
                                'images, sigma %.3g, full iteration (decode+CIDEr-D+ranks+noise sum+Adam)'
-                               % (P, P_local, B, args.sigma) + (", 'bu' fc features" if args.bu else ''),
+                               % (P, P_local, B, args.sigma) + (", 'bu' fc features" if args.bu else '')
+                               + (', fitness %s' % args.fitness if args.fitness != 'greedy' else ''),
                    'population': P, 'members_per_gpu': P_local, 'batch_size': B, 'seq_length': 16,
                    'vocab_size': 9487, 'parallelism': 'population-sharded x%d, RCCL all-gather + all-reduce'
                    % world},
