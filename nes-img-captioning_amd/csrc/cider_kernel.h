@@ -35,9 +35,10 @@ extern "C" hipError_t nicnes_launch_cook_refs(const int32_t* ref_tokens, int n_r
 extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int B, const CiderTables* tb,
                                                hipStream_t stream);
 // lp (nullable) [n_cand, B, T] per-step log-probs; crit = fitness criterion (nicnes_set_fitness_mode)
+// scores: scratch [n_cand, B] fp64 (per-row CIDEr-D, reduced by a second kernel)
 extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
                                               const int32_t* img_ref_start, const float* lp, int crit,
-                                              double* fitness_out, hipStream_t stream);
+                                              double* scores, double* fitness_out, hipStream_t stream);
 extern "C" hipError_t nicnes_launch_cider(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
                                           const int32_t* img_ref_start, const float* lp, int crit,
                                           double* fitness_out, hipStream_t stream);

@@ -310,15 +310,18 @@ __global__ __launch_bounds__(64) void nicnes_img_ngram_kernel(const int32_t* img
 }
 
 // candidates scored against the image table: one probe per distinct n-gram, then the per-reference
-// weights are consecutive doubles (same arithmetic and order as nicnes_cider_kernel)
+// weights are consecutive doubles (same arithmetic and order as nicnes_cider_kernel).
+// Grid (candidate, row block of CIDER_IMG_ROWS): the probe chains are latency-bound, so each
+// candidate's rows are spread over several workgroups; per-row scores go to `scores` [n_cand, B]
+// and nicnes_cider_finish_kernel reduces them in row order, as the single-workgroup form did.
+#define CIDER_IMG_ROWS 32
 __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* seq, int B, int T, CiderTables tb,
-                                                               const int32_t* img_ref_start, const float* lp,
-                                                               int crit, double* fitness_out) {
-    __shared__ double row_score[1024];
+                                                               const int32_t* img_ref_start, double* scores) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int cand = blockIdx.x;
+    const int b_end = min(B, (int)(blockIdx.y + 1) * CIDER_IMG_ROWS);
     const double sigma2x2 = 2.0 * 6.0 * 6.0;
-    for (int b = wave; b < B; b += 4) {
+    for (int b = (int)blockIdx.y * CIDER_IMG_ROWS + wave; b < b_end; b += 4) {
         const int32_t* row = seq + ((size_t)cand * B + b) * T;
         const NgramLane g = ngram_lane(row, T, lane, tb);
         const double nh = sqrt(seg_sum(g.first ? g.vec * g.vec : 0.0));
@@ -353,12 +356,17 @@ __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* se
             double avg = score / 4.0;
             avg /= (double)(r1 - r0);
             avg *= 10.0;
-            row_score[b] = avg;
+            scores[(size_t)cand * B + b] = avg;
         }
     }
-    __syncthreads();
-    finish_fitness(row_score, seq + (size_t)cand * B * T, lp ? lp + (size_t)cand * B * T : nullptr, B, T, crit,
-                   fitness_out + cand);
+}
+
+__global__ __launch_bounds__(256) void nicnes_cider_finish_kernel(const int32_t* seq, int B, int T,
+                                                                  const double* scores, const float* lp, int crit,
+                                                                  double* fitness_out) {
+    const int cand = blockIdx.x;
+    finish_fitness(scores + (size_t)cand * B, seq + (size_t)cand * B * T, lp ? lp + (size_t)cand * B * T : nullptr,
+                   B, T, crit, fitness_out + cand);
 }
 
 extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int B, const CiderTables* tb,
@@ -369,9 +377,11 @@ extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int
 
 extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
                                               const int32_t* img_ref_start, const float* lp, int crit,
-                                              double* fitness_out, hipStream_t stream) {
-    if (B > 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(nicnes_cider_img_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, *tb, img_ref_start, lp,
-                       crit, fitness_out);
+                                              double* scores, double* fitness_out, hipStream_t stream) {
+    if (B > 1024 || n_cand < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(nicnes_cider_img_kernel, dim3(n_cand, (B + CIDER_IMG_ROWS - 1) / CIDER_IMG_ROWS), dim3(256), 0,
+                       stream, seq, B, T, *tb, img_ref_start, scores);
+    hipLaunchKernelGGL(nicnes_cider_finish_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, (const double*)scores,
+                       lp, crit, fitness_out);
     return hipGetLastError();
 }

@@ -65,6 +65,7 @@ struct nicnes_handle {
     uint64_t* nidx = nullptr;
     int32_t* seq = nullptr;
     float* lp = nullptr;              // per-step log-probs for the greedy_* criteria
+    double* row_scores = nullptr;     // per-row CIDEr-D of the image-table scorer [2 * max_members, max_batch]
     int fitness_mode = 0;             // nicnes_set_fitness_mode (0 = 'greedy')
     float* dscratch = nullptr;
     int32_t* stats = nullptr;
@@ -187,6 +188,7 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
     if (!rc) rc = dalloc(h, &h->nidx, MM);
     if (!rc) rc = dalloc(h, &h->seq, MM * 2 * MB * T);
     if (!rc) rc = dalloc(h, &h->lp, MM * 2 * MB * T);
+    if (!rc) rc = dalloc(h, &h->row_scores, MM * 2 * MB);
     {
         const char* fe = getenv("NICNES_FORCE_EXACT");
         h->force_exact = (fe && fe[0] == '1') ? 1 : 0;
@@ -215,7 +217,7 @@ int nicnes_destroy(nicnes_handle* h) {
     if (!h) return NICNES_OK;
     (void)hipSetDevice(h->device);
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
-                    h->ref_norm, h->nidx, h->seq, h->lp, h->dscratch, h->stats, h->partials, h->norms,
+                    h->ref_norm, h->nidx, h->seq, h->lp, h->row_scores, h->dscratch, h->stats, h->partials, h->norms,
                     h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -429,7 +431,7 @@ int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begi
     CiderTables tb = tables_of(h);
     if (h->img_tables)
         HIPC(h, nicnes_launch_cider_img(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, p.lp,
-                                         h->fitness_mode, fitness_out, s));
+                                         h->fitness_mode, h->row_scores, fitness_out, s));
     else
         HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, p.lp,
                                          h->fitness_mode, fitness_out, s));
