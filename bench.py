@@ -35,6 +35,18 @@ def decode_flops_per_member(B, V1=9488, E=128, R=128, F=2048):
     return 2 * B * per_row
 
 
+def step_noise_bytes_per_member(B, T=16, V1=9488, E=128, R=128):
+    """Algorithmic HBM bytes of one member over the T + 2 step launches of a decode: the member's own
+    noise rows, read once per use (they cannot stay on chip between steps): the logit matrix + bias
+    at each of the T logit steps, the i2h/h2h matrices + biases at each of the T + 1 cells, and the
+    2 x B embedding rows of each step's tokens (T - 1 token steps; the BOS step reads one row).
+    Base theta is shared by every member (L2/MALL) and not counted."""
+    logit = V1 * (R + 1) * 4
+    cell = 2 * 5 * R * (E + 1) * 4
+    emb = 2 * B * E * 4
+    return T * logit + (T + 1) * cell + (T - 1) * emb + E * 4
+
+
 def step_flops_per_member(B, V1=9488, E=128, R=128):
     """The part of decode_flops_per_member done by nicnes_decode_step_kernel: the 16 logit GEMMs and
     the 17 LSTM cells' gate sums, i2h and h2h halves (the img kernel does the image projection)."""
@@ -173,6 +185,9 @@ def main():
                      'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,
                      'kernel_ms_per_launch': round(step_ms, 4), 'launches_per_step': n_step,
                      'algorithmic_flop_per_launch': step_flop,
+                     'algorithmic_bytes_per_launch': step_noise_bytes_per_member(B) * P_local / n_step,
+                     'traffic_over_algorithmic': (round(traffic / (step_noise_bytes_per_member(B) * P_local / n_step), 3)
+                                                  if traffic else None),
                      'decode': {'ms_per_step': round(dec_s * 1e3, 3), 'algorithmic_flop': flops,
                                 'tflops': round(flops / dec_s / 1e12, 3),
                                 'frac': round(flops / dec_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
