@@ -337,6 +337,22 @@ int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t
     if (!h->df_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_df_table first");
     if (((uintptr_t)fc & 15u) != 0) return fail(h, NICNES_ERR_INVALID, "fc must be 16-byte aligned");
     HIPC(h, hipSetDevice(h->device));
+    // reference ranges: CiderD asserts every image has references (len(ref) > 0, upstream
+    // cider_scorer); ranges must tile [0, n_refs)
+    std::vector<int32_t> st((size_t)B + 1);
+    HIPC(h, hipMemcpyAsync(st.data(), img_ref_start, st.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
+                           (hipStream_t)stream));
+    HIPC(h, hipStreamSynchronize((hipStream_t)stream));
+    int maxr = 0;
+    bool ok = st[0] == 0 && st[B] == n_refs;
+    for (int b = 0; b < B && ok; ++b) {
+        ok = st[b + 1] > st[b];
+        maxr = std::max(maxr, st[b + 1] - st[b]);
+    }
+    if (!ok) {
+        h->batch_set = false;
+        return fail(h, NICNES_ERR_INVALID, "img_ref_start must start at 0, end at n_refs and give every image >= 1 reference");
+    }
     h->fc = fc;
     h->B = B;
     h->n_refs = n_refs;
@@ -345,15 +361,7 @@ int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t
     HIPC(h, nicnes_launch_cook_refs(ref_tokens, n_refs, h->cfg.seq_length, &tb, (hipStream_t)stream));
     // per-image n-gram tables when every image has at most IMG_MAXR references (else the
     // per-reference scan kernel scores the candidates)
-    {
-        std::vector<int32_t> st((size_t)B + 1);
-        HIPC(h, hipMemcpyAsync(st.data(), img_ref_start, st.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
-                               (hipStream_t)stream));
-        HIPC(h, hipStreamSynchronize((hipStream_t)stream));
-        int maxr = 0;
-        for (int b = 0; b < B; ++b) maxr = std::max(maxr, st[b + 1] - st[b]);
-        h->img_tables = maxr <= IMG_MAXR;
-    }
+    h->img_tables = maxr <= IMG_MAXR;
     if (h->img_tables) {
         HIPC(h, hipMemsetAsync(h->img_vr, 0, (size_t)B * IMG_ROWS * IMG_MAXR * sizeof(double), (hipStream_t)stream));
         HIPC(h, nicnes_launch_img_ngrams(img_ref_start, B, &tb, (hipStream_t)stream));

@@ -133,6 +133,8 @@ class Engine:
         zero-padded label rows (data['gts'], /root/reference/src/captioning/dataloader.py:162)."""
         fc_t = self._dev(fc, torch.float32)
         B = fc_t.shape[0]
+        if len(gts) != B:
+            raise ValueError('gts has %d images, fc has %d rows' % (len(gts), B))
         rows, start = [], [0]
         for g in gts:
             g = np.asarray(g, np.int32).reshape(-1, self.cfg.seq_length)

@@ -172,6 +172,26 @@ def test_fitness_criteria_match_oracle(eng, mode, n_refs):
     assert fit.max() > 0.0
 
 
+def test_set_batch_rejects_images_without_references(eng):
+    """CiderD asserts len(ref) > 0 for every image (upstream cider_scorer); the engine refuses such a
+    batch with a status instead of scoring a 0/0, and a good batch loads again afterwards."""
+    import nicnes
+    dims = O.Dims()
+    fc = np.random.Generator(np.random.PCG64(5)).standard_normal((4, dims.F)).astype(np.float32)
+    gts = [np.ones((2, 16), np.int32), np.zeros((0, 16), np.int32), np.ones((1, 16), np.int32),
+           np.ones((3, 16), np.int32)]
+    eng.set_theta(O.make_theta(dims, 0, 4.0, 0.1))
+    with pytest.raises(nicnes.NicnesError):
+        eng.set_batch(fc, gts)
+    with pytest.raises(nicnes.NicnesError):
+        eng.evaluate(1, 0, 1, SIGMA)                       # no batch loaded
+    with pytest.raises(ValueError):
+        eng.set_batch(fc, gts[:3])
+    gts[1] = np.ones((1, 16), np.int32)
+    eng.set_batch(fc, gts)
+    assert np.isfinite(eng.evaluate(1, 0, 1, SIGMA).cpu().numpy()).all()
+
+
 def test_fitness_mode_rejects_unsupported(eng):
     import nicnes
     for bad in ('sample', 'self_critical', 'sc_loss', 7):
