@@ -114,14 +114,20 @@ def main():
     import nicnes.synthetic as S
     from nicnes.population import PopulationRunner
 
-    torch.cuda.set_device(local_rank)
+    # rehearsal knobs for a one-GPU box (never set by the driver): every rank on cuda:0 over gloo
+    backend = os.environ.get('NICNES_BENCH_BACKEND', 'nccl')
+    dev = 0 if os.environ.get('NICNES_BENCH_SHARE_GPU') == '1' else local_rank
+    torch.cuda.set_device(dev)
     group = None
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
+        else:
+            dist.init_process_group(backend)
     P_local = args.pop_per_gpu
     P = P_local * world
     eng = nicnes.Engine(max_batch=B, max_members=P_local, noise_len=args.noise_len, noise_seed=0,
-                        device=local_rank)
+                        device=dev)
     S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu)
     eng.set_fitness_mode(args.fitness)
     runner = PopulationRunner(eng, P, args.sigma, l2coeff=1e-7, stepsize=1e-3, rank=rank, world_size=world,
