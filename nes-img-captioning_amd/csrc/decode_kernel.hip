@@ -275,7 +275,7 @@ __device__ __forceinline__ void mfma_stage64(const float* w, const float* bias, 
 
 // cell stage: chain a = i2h tile (stage rows 0-31) over B = x, chain b = h2h tile (rows 32-63)
 // over B = h; k chunks [T0, T1) of 32 (init: start from the bias)
-template <int T0, int T1>
+template <int T0, int T1, bool H = true>
 __device__ __forceinline__ void mfma_xh_part(const float* w, const float* bias, const float (&Bx)[64],
                                              const float (&Bh)[64], int lane, f32x16& acc0, f32x16& acc1) {
     const int hh = lane >> 5;
@@ -296,7 +296,7 @@ __device__ __forceinline__ void mfma_xh_part(const float* w, const float* bias, 
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) {
             acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bx[16 * T + jj], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bh[16 * T + jj], acc1, 0, 0, 0);
+            if (H) acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bh[16 * T + jj], acc1, 0, 0, 0);
         }
     }
 }
@@ -691,7 +691,10 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         if (m < 19) stage64_load(csrc(m + 1), c.wave * 64 + lane_fresh(), s64);
         const float* buf = lds + ((m + b0) & 1) * STAGE64_FLOATS;
         f32x16 a0, a1;
-        mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
+        if (t < 0)      // h = 0 before the first cell: h2h(h) is its bias (fma(w, 0, acc) == acc)
+            mfma_xh_part<0, 4, false>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
+        else
+            mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
         fold(m, a0 + a1, cpre);                                  // i2h(x) + h2h(h), nets.py:109-111
         if (m < 19) stage64_store(lds + ((m + 1 + b0) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
         __syncthreads();
