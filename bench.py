@@ -54,6 +54,16 @@ def step_flops_per_member(B, V1=9488, E=128, R=128):
     return 2 * B * per_row
 
 
+def logit_flops_per_member(B, V1=9488, R=128, T=16):
+    """The logit GEMMs of one member (2 decodes of B rows, T steps): the split path's logit kernel."""
+    return 2 * B * T * 2 * R * V1
+
+
+def logit_noise_bytes_per_member(V1=9488, R=128):
+    """A member's logit-matrix + bias noise rows, read once per logit launch."""
+    return V1 * (R + 1) * 4
+
+
 def cpu_baseline(args, B):
     """The reference CPU worker path (torch-CPU restatement, oracle/ref_worker.py) on this box's
     host cores: one single-threaded process per core, one member per process."""
@@ -94,6 +104,8 @@ def main():
     ap.add_argument('--fitness', default='greedy', help="policy_options.fitness: greedy (mscoco_nes.json) or "
                     "greedy_logprob / greedy_expprob / greedy_linprob / greedy_avgprob")
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--decode-split', type=int, default=0, help='force S logit workgroups per member (0 = auto)')
+    ap.add_argument('--decode-rows', type=int, default=0, help='force 4 (128-row) or 2 (64-row) slabs (0 = auto)')
     ap.add_argument('--cpu-cores', type=int, default=16)
     ap.add_argument('--cpu-members-per-core', type=int, default=1)
     args = ap.parse_args()
@@ -130,6 +142,7 @@ def main():
                         device=dev)
     S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu)
     eng.set_fitness_mode(args.fitness)
+    eng.set_decode_split(args.decode_split, args.decode_rows)
     runner = PopulationRunner(eng, P, args.sigma, l2coeff=1e-7, stepsize=1e-3, rank=rank, world_size=world,
                               group=group)
     it = 1
@@ -160,19 +173,29 @@ def main():
     value = P * args.steps / dt
     dec_s = float(np.mean(dec_ms)) / 1e3
     flops = decode_flops_per_member(B) * P_local
-    # dominant kernel: the step kernel (logits + token + next LSTM cell), T + 2 launches per
-    # evaluate; per-launch figures are the evaluate's totals / launches (what rocprofv3 --stats
+    # dominant kernel: the fused step kernel (logits + token + next LSTM cell, T + 2 launches per
+    # evaluate) or, on the split path (members x slabs below the CU count), the logit kernel (T
+    # launches); per-launch figures are the evaluate's totals / launches (what rocprofv3 --stats
     # averages over the same launches)
-    n_step = phases[-1]['step_launches']
-    step_ms = float(np.mean([ph['step_ms'] for ph in phases])) / n_step
-    step_flop = step_flops_per_member(B) * P_local / n_step
+    ph = phases[-1]
+    G, nslabs, S_split = eng.decode_shape(B, P_local)
+    if ph['step_launches']:
+        kname, n_step = 'nicnes_decode_step_kernel', ph['step_launches']
+        step_ms = float(np.mean([q['step_ms'] for q in phases])) / n_step
+        step_flop = step_flops_per_member(B) * P_local / n_step
+        alg_bytes = step_noise_bytes_per_member(B) * P_local / n_step
+    else:
+        kname, n_step = 'nicnes_decode_logit_kernel<%d>' % G, ph['logit_launches']
+        step_ms = float(np.mean([q['logit_ms'] for q in phases])) / n_step
+        step_flop = logit_flops_per_member(B) * P_local / n_step
+        alg_bytes = logit_noise_bytes_per_member() * P_local / n_step
     achieved = step_flop / (step_ms / 1e3) / 1e12
     traffic = None
     pmc = os.path.join(REPO, 'profiles', 'r01_decode_pmc.json')
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and kname == 'nicnes_decode_step_kernel' and P_local == 512 and B == 128:
         with open(pmc) as f:
             rec = json.load(f)
-        if rec.get('kernel') == 'nicnes_decode_step_kernel':
+        if rec.get('kernel') == kname:
             traffic = rec.get('hbm_bytes_per_launch')
     out = {
         'metric': METRIC, 'value': round(value, 3), 'unit': 'members/s', 'n_gpus': world, 'steps': args.steps,
@@ -186,20 +209,21 @@ def main():
                    'population': P, 'members_per_gpu': P_local, 'batch_size': B, 'seq_length': 16,
                    'vocab_size': 9487, 'parallelism': 'population-sharded x%d, RCCL all-gather + all-reduce'
                    % world},
-        'roofline': {'bound': 'mfma', 'kernel': 'nicnes_decode_step_kernel', 'achieved': round(achieved, 3),
+        'roofline': {'bound': 'mfma', 'kernel': kname, 'achieved': round(achieved, 3),
                      'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                      'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,
                      'kernel_ms_per_launch': round(step_ms, 4), 'launches_per_step': n_step,
                      'algorithmic_flop_per_launch': step_flop,
-                     'algorithmic_bytes_per_launch': step_noise_bytes_per_member(B) * P_local / n_step,
-                     'traffic_over_algorithmic': (round(traffic / (step_noise_bytes_per_member(B) * P_local / n_step), 3)
-                                                  if traffic else None),
+                     'algorithmic_bytes_per_launch': alg_bytes,
+                     'traffic_over_algorithmic': (round(traffic / alg_bytes, 3) if traffic else None),
                      'decode': {'ms_per_step': round(dec_s * 1e3, 3), 'algorithmic_flop': flops,
                                 'tflops': round(flops / dec_s / 1e12, 3),
                                 'frac': round(flops / dec_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
-                                'img_ms': round(float(np.mean([ph['img_ms'] for ph in phases])), 3),
-                                'cell_only_ms': round(float(np.mean([ph['cell_only_ms'] for ph in phases])), 3),
-                                'step_ms': round(step_ms * n_step, 3)}},
+                                'img_ms': round(float(np.mean([q['img_ms'] for q in phases])), 3),
+                                'cell_only_ms': round(float(np.mean([q['cell_only_ms'] for q in phases])), 3),
+                                'step_ms': round(ph['step_ms'], 3), 'logit_ms': round(ph['logit_ms'], 3),
+                                'cell_ms': round(ph['cell_ms'], 3),
+                                'shape': {'row_groups': G, 'slabs': nslabs, 'logit_split': S_split}}},
         'cpu_baseline': cpu,
         'tie_fallbacks': eng.stats()['tie_fallbacks'],
         'update_ratio': ratio,

@@ -1,6 +1,7 @@
 // Internal (non-ABI) launch interfaces of the engine's kernels.
 #pragma once
-#define SCR_SLOTS (64 + 64 + 64 + 1)   // per lane: c | h' | x of t = 0 | unfinished
+#define SCR_SLOTS (64 + 64 + 64 + 1 + 64)   // per lane: c | h' | x of t = 0 | unfinished | h' (odd parity, split path)
+#define PART_FLOATS (8 * 7 * 64)             // split path: partial greedy state of one logit workgroup (8 waves x 7 x 64 lanes)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -11,18 +12,33 @@ struct DecodeParams {
     const float* fc;             // unique-image fc features [B, F]
     int32_t* seq;                // out: [members, 2, B, T] greedy tokens (masked after the first 0)
     float* lp;                   // out (nullable): [members, 2, B, T] log-prob of the greedy token (nets.py:208,241)
-    float* scratch;              // nicnes_decode_scratch_floats(): lane-private c | h' | x0 | unfinished
+    float* scratch;              // nicnes_decode_scratch_floats(): lane-private c | h' | x0 | unfinished | h' (odd)
     int32_t* stats;              // [0] = exact-pass fallbacks (atomic)
-    int32_t* alive;              // [members * slabs]: 0 once every row of the workgroup finished
+    int32_t* alive;              // fused path: [members * slabs], 0 once every row of the workgroup finished
+    int32_t* alive2;             // split path: [2][alive_stride] by step parity
+    float* part;                 // split path: [members * slabs * S] x PART_FLOATS partial greedy states
     float sigma;
     int32_t force_exact;         // test hook (NICNES_FORCE_EXACT=1): every step takes the exact tie pass
     int32_t B, F, V1, T;
+    int32_t G;                   // row groups per slab: 4 (128-row slabs) or 2 (64-row slabs)
+    int32_t S;                   // logit workgroups per member slab (1 + G = 4: the fused step kernel)
+    int32_t alive_stride;
     int64_t D;
     int64_t off_img_w, off_img_b, off_emb_w, off_log_w, off_log_b, off_i2h_w, off_i2h_b, off_h2h_w, off_h2h_b;
 };
 
-// evs (nullable): T + 4 events, recorded before the first launch and after every launch (img, step -1..T)
+// launch kinds recorded next to the timing events
+#define DK_IMG 0
+#define DK_STEP 1        // fused step kernel (logits of t + cell of t + 1)
+#define DK_CELL 2        // split path: token merge of t + cell of t + 1
+#define DK_LOGIT 3       // split path: logits of t over one vocabulary range
+
+// evs (nullable): up to DECODE_MAX_EVENTS events, recorded before the first launch and after every
+// launch; kinds[k] (k >= 1) is the kind of the launch that event k follows. Returns the launch count
+// in *n_launch.
 #define DECODE_MAX_EVENTS 64
+extern "C" hipError_t nicnes_decode_init();
 extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,
-                                           hipEvent_t* evs);
-extern "C" size_t nicnes_decode_scratch_floats(int member_count, int nslabs);
+                                           hipEvent_t* evs, int* kinds, int* n_launch);
+// lane scratch for up to member_count members x row_waves 32-row waves of one sign
+extern "C" size_t nicnes_decode_scratch_floats(int member_count, int row_waves_per_member);

@@ -426,20 +426,66 @@ __device__ __forceinline__ Ctx make_ctx(const DecodeParams& p) {
     return c;
 }
 
+// ---- workgroup roles of the img kernel and the split path -----------------------------------
+// grid (q, member, slab). G = 4: wave w = sign (w >> 2) x 32-row group (w & 3) of a 128-row slab.
+// G = 2 (64-row slabs, B <= 64): wave w = sign (w >> 2) x group ((w >> 1) & 1) x tile half (w & 1);
+// the two halves of a (sign, group) pair share rows and run one 32-row MFMA tile each.
+// w and w + 4 (opposite signs, same rows / tile half) share a SIMD in both layouts.
+template <int G>
+struct SCtx {
+    int tid, lane, wave, sgn, grp, hf, hh, member, slab, q, wg, b, bc;
+    bool row_valid;
+    float sigma;
+    rsrc_t theta_r, noise_r, scr_r;
+};
+
+template <int G>
+__device__ __forceinline__ SCtx<G> make_sctx(const DecodeParams& p) {
+    SCtx<G> c;
+    c.tid = threadIdx.x;
+    c.lane = c.tid & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(c.tid >> 6);
+    c.sgn = c.wave >> 2;
+    c.grp = G == 4 ? (c.wave & 3) : ((c.wave >> 1) & 1);
+    c.hf = G == 4 ? 0 : (c.wave & 1);
+    c.hh = c.lane >> 5;
+    c.q = blockIdx.x;
+    c.member = blockIdx.y;
+    c.slab = blockIdx.z;
+    c.wg = c.member * gridDim.z + c.slab;
+    c.b = c.slab * (32 * G) + c.grp * 32 + (c.lane & 31);
+    c.row_valid = c.b < p.B;
+    c.bc = c.row_valid ? c.b : 0;
+    c.sigma = p.sigma;
+    const uint64_t nidx = p.noise_idx[c.member];
+    const uint32_t Dbytes = 4u * (uint32_t)p.D;
+    c.theta_r = make_rsrc(p.theta, Dbytes);
+    c.noise_r = make_rsrc(p.noise + nidx, Dbytes);
+    // lane scratch per (slab, sign, row group); G = 4 gives the fused kernel's (wg * 8 + wave)
+    float* wscr = p.scratch + ((size_t)c.wg * (2 * G) + c.sgn * G + c.grp) * (SCR_SLOTS * 64);
+    c.scr_r = make_rsrc(wscr, SCR_SLOTS * 64 * 4);
+    return c;
+}
+
 // ========== t = 0 input: x = img_embed(fc) (nets.py:194-195) ====================================
+// grid (Sc, members, slabs): workgroup q computes the 32-unit blocks [q * 4/Sc, (q+1) * 4/Sc) of x
+// (Sc = 1: all four, the fused path). With G = 2 the tile-half-1 waves only help stage.
+template <int G>
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParams p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const Ctx c = make_ctx(p);
+    const SCtx<G> c = make_sctx<G>(p);
     PROF_MARK(80);
     const rsrc_t fc_r = make_rsrc(p.fc, 4u * (uint32_t)p.B * (uint32_t)p.F);
     const uint32_t lo = 4u * c.lane;
+    const bool mm = G == 4 || c.hf == 0;
     StageRegs sr;
     f32x16 accU[4];
     const int nK = p.F >> 7;
-    const int ntile = nK * 4;
+    const int nb = 4 / (int)gridDim.x, U0 = nb * c.q;
+    const int ntile = nK * nb;
     auto desc = [&](int n) {
         TileDesc d;
-        d.w_off = (uint32_t)p.off_img_w; d.ld = p.F; d.row0 = 32 * (n & 3); d.nvalid = 32; d.k0 = 128 * (n >> 2);
+        d.w_off = (uint32_t)p.off_img_w; d.ld = p.F; d.row0 = 32 * (U0 + n % nb); d.nvalid = 32; d.k0 = 128 * (n / nb);
         d.b_off = (uint32_t)p.off_img_b; d.pad_bias = 0.f;
         return d;
     };
@@ -450,21 +496,29 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
         const uint32_t frow = 4u * (uint32_t)(c.bc * p.F + 128 * kc + 4 * c.hh);
 #pragma unroll
         for (int U = 0; U < 4; ++U) {
-            const int n = kc * 4 + U;
-            if (n + 1 < ntile) stage_load(c.theta_r, c.noise_r, desc(n + 1), c.tid, sr);
-            const float* buf = lds + (n & 1) * STAGE_FLOATS;
-            if (kc == 0) accU[U] = bias_init(buf + 2 * SIGN_FLOATS + 32 * c.sgn, c.hh);
-            accU[U] = mfma_tile_fc(accU[U], buf + c.sgn * SIGN_FLOATS, fc_r, frow, c.lane);
-            if (n + 1 < ntile) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), c.sigma, c.tid, sr);
-            __syncthreads();
+            if (U < nb) {
+                const int n = kc * nb + U;
+                if (n + 1 < ntile) stage_load(c.theta_r, c.noise_r, desc(n + 1), c.tid, sr);
+                const float* buf = lds + (n & 1) * STAGE_FLOATS;
+                if (mm) {
+                    if (kc == 0) accU[U] = bias_init(buf + 2 * SIGN_FLOATS + 32 * c.sgn, c.hh);
+                    accU[U] = mfma_tile_fc(accU[U], buf + c.sgn * SIGN_FLOATS, fc_r, frow, c.lane);
+                }
+                if (n + 1 < ntile) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), c.sigma, c.tid, sr);
+                __syncthreads();
+            }
         }
     }
+    if (mm) {
 #pragma unroll
-    for (int U = 0; U < 4; ++U)
+        for (int U = 0; U < 4; ++U)
+            if (U < nb) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) st1(c.scr_r, lo, X_SLOT(16 * U + r), accU[U][r]);
-    st1(c.scr_r, lo, U_SLOT, 1.0f);
-    if (c.tid == 0) p.alive[c.wg] = 1;
+                for (int r = 0; r < 16; ++r) st1(c.scr_r, lo, X_SLOT(16 * (U0 + U) + r), accU[U][r]);
+            }
+        st1(c.scr_r, lo, U_SLOT, 1.0f);
+    }
+    if (c.q == 0 && c.tid == 0) p.alive[c.wg] = 1;
     PROF_MARK(81);
 }
 
@@ -702,30 +756,424 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
     PROF_MARK(2 * (t + 1) + 1);
 }
 
-extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,
-                                           hipEvent_t* evs) {
-    const size_t lds64 = (size_t)(2 * STAGE64_FLOATS) * sizeof(float);
-    const size_t lds32 = (size_t)(2 * STAGE_FLOATS) * sizeof(float);
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)nicnes_decode_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds64);
+// ========== split path: one member step over several workgroups =================================
+// When members x slabs workgroups cannot fill the chip (64 members per GPU: configs[1] pop=64 and
+// the per-GPU slice of configs[4]), each step t is split in two launches:
+//   nicnes_decode_logit_kernel  grid (S, members, slabs): the logit GEMM of step t over vocabulary
+//       stage range q; each lane leaves its rows' partial greedy state (online max and exp-sum, the
+//       last two left-to-right records, the largest evicted record) in HBM;
+//   nicnes_decode_cell_kernel   grid (Sc, members, slabs), Sc = min(S, 4): every workgroup of the
+//       member merges the S partials into the same token (the fused kernel's candidate rule holds on
+//       any partition of the vocabulary scanned in index order: the first in-window id of a range is
+//       one of that range's last two records unless an evicted record is in the window too, which
+//       sends the row to the exact pass), then runs the gate tiles of its 4/Sc unit blocks.
+// h crosses launches in two parity slots: cell(t) reads h_t and writes its blocks of h_{t+1}. The
+// unfinished flag of a row is seq[t-2] != 0 (it = tok * unfinished, nets.py:236-241). The q index
+// is blockIdx.x, so consecutive workgroups (round-robin over the 8 XCDs) take different vocabulary
+// ranges and each XCD's L2 holds a quarter of the logit matrix at S = 4.
+#define HP_SLOT(par, s) (4u * 64u * (uint32_t)((par) ? 193 + (s) : 64 + (s)))   // h' by step parity
+
+__device__ __forceinline__ float* part_ptr(const DecodeParams& p, int wg, int q, int wave) {
+    return p.part + (((size_t)wg * p.S + q) * 8 + wave) * (7 * 64);
+}
+
+// epilogue of one 32-row logit tile (G = 2: one tile per wave); P0 holds vocab vbase + (r&3) + 8(r>>2)
+__device__ __forceinline__ void epilogue32(RowState& st, const f32x16& P0, int vbase) {
+    const float g0 = max4(P0, 0), g1 = max4(P0, 1), g2 = max4(P0, 2), g3 = max4(P0, 3);
+    const float tmax = fmaxf(fmaxf(g0, g1), fmaxf(g2, g3));
+    const float mnew = fmaxf(st.m, tmax);
+    const float ml = mnew * LOG2E;
+    float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(P0[r], LOG2E, -ml));
+    st.s = s;
+    st.m = mnew;
+    if (__any(tmax > st.r1v)) {
+        if (__any(g0 > st.r1v)) records4<0>(st, P0, vbase);
+        if (__any(g1 > st.r1v)) records4<1>(st, P0, vbase);
+        if (__any(g2 > st.r1v)) records4<2>(st, P0, vbase);
+        if (__any(g3 > st.r1v)) records4<3>(st, P0, vbase);
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(NTHREADS) void nicnes_decode_logit_kernel(DecodeParams p, int t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const SCtx<G> c = make_sctx<G>(p);
+    if (t > 1 && p.alive2[((t - 1) & 1) * p.alive_stride + c.wg] == 0) return;
+    const uint32_t lo = 4u * c.lane;
+    const int nst = (p.V1 + 63) >> 6, S = (int)gridDim.x;
+    const int s0 = c.q * nst / S, s1 = (c.q + 1) * nst / S;
+    const uint64_t nidx = p.noise_idx[c.member];
+    float hB[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, HP_SLOT(t & 1, i));
+#pragma unroll
+    for (int i = 0; i < 64; ++i) pin(hB[i]);
+    RowState st;
+    row_state_init(st);
+    if (s1 > s0) {
+        const rsrc_t lw_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
+        const rsrc_t lz_r = make_rsrc(p.noise + nidx + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
+        const rsrc_t lbw_r = make_rsrc(p.theta + p.off_log_b, 4u * (uint32_t)p.V1);
+        const rsrc_t lbz_r = make_rsrc(p.noise + nidx + p.off_log_b, 4u * (uint32_t)p.V1);
+        auto lsrc = [&](int s) {                                 // logit rows 64s .. 64s+63
+            StageSrc Sx;
+            Sx.w_r = lw_r; Sx.z_r = lz_r; Sx.b_r = lbw_r; Sx.bz_r = lbz_r;
+            Sx.so_a = 32768u * (uint32_t)s; Sx.so_b = Sx.so_a + 16384u;
+            Sx.bso = 256u * (uint32_t)s; Sx.bda = 0u; Sx.bdb = 128u;
+            Sx.valid = p.V1 - 64 * s;
+            return Sx;
+        };
+        Stage64Regs s64;
+        stage64_load(lsrc(s0), c.wave * 64 + lane_fresh(), s64);
+        stage64_store(lds, lsrc(s0).valid, c.sigma, c.wave * 64 + lane_fresh(), s64);
+        __syncthreads();
+        f32x16 prev0, prev1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { prev0[r] = NEG_INF; prev1[r] = NEG_INF; }
+        for (int s = s0; s < s1; ++s) {
+            const int sn = min(s + 1, s1 - 1);
+            stage64_load(lsrc(sn), c.wave * 64 + lane_fresh(), s64);
+            const float* buf = lds + ((s - s0) & 1) * STAGE64_FLOATS;
+            const float* wsg = buf + c.sgn * (64 * LDS_ROW);
+            const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * c.sgn;
+            f32x16 acc0, acc1;
+            if constexpr (G == 4) {
+                if (c.sgn == 0) {
+                    mfma_stage64(wsg, bsg, hB, lane_fresh(), acc0, acc1);
+                    epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
+                } else {
+                    epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
+                    mfma_stage64(wsg, bsg, hB, lane_fresh(), acc0, acc1);
+                }
+            } else {
+                const float* w1 = wsg + 32 * c.hf * LDS_ROW;     // this wave's 32-row tile of the stage
+                const float* b1 = bsg + 32 * c.hf;
+                if (c.sgn == 0) {
+                    acc0 = mfma_tile(bias_init(b1, lane_fresh() >> 5), w1, hB, lane_fresh());
+                    epilogue32(st, prev0, 64 * (s - 1) + 32 * c.hf + 4 * (lane_fresh() >> 5));
+                } else {
+                    epilogue32(st, prev0, 64 * (s - 1) + 32 * c.hf + 4 * (lane_fresh() >> 5));
+                    acc0 = mfma_tile(bias_init(b1, lane_fresh() >> 5), w1, hB, lane_fresh());
+                }
+            }
+            stage64_store(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, c.sigma, c.wave * 64 + lane_fresh(), s64);
+            __syncthreads();
+            prev0 = acc0;
+            if constexpr (G == 4) prev1 = acc1;
+        }
+        if constexpr (G == 4)
+            epilogue64(st, prev0, prev1, 64 * (s1 - 1) + 4 * (lane_fresh() >> 5));
+        else
+            epilogue32(st, prev0, 64 * (s1 - 1) + 32 * c.hf + 4 * (lane_fresh() >> 5));
+    }
+    float* pb = part_ptr(p, c.wg, c.q, c.wave) + lane_fresh();
+    pb[0] = st.m;
+    pb[64] = st.s;
+    pb[128] = st.r0v;
+    pb[192] = __builtin_bit_cast(float, st.r0i);
+    pb[256] = st.r1v;
+    pb[320] = __builtin_bit_cast(float, st.r1i);
+    pb[384] = st.ev;
+}
+
+template <int G>
+__global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodeParams p, int t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const SCtx<G> c = make_sctx<G>(p);
+    const bool lead = c.q == 0 && c.tid == 0;
+    if (t > 1 && p.alive2[((t - 1) & 1) * p.alive_stride + c.wg] == 0) {
+        if (lead) p.alive2[(t & 1) * p.alive_stride + c.wg] = 0;   // keep the parity chain current
+        return;
+    }
+    const uint32_t lo = 4u * c.lane;
+    const bool folder = G == 4 || c.hf == 0;       // waves that own the rows' token and the cell fold
+    float hB[64];
+    if (t < 0) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) hB[i] = 0.f;               // h = 0 before the first cell
+    } else {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, HP_SLOT(t & 1, i));
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) pin(hB[i]);
+    int it = 0;                                   // token fed to the next cell (0 = BOS at t = 0)
+    if (t >= 1) {
+        // ---- merge the S partial states of each row (lane halves combined last, as the fused kernel)
+        float m = 0.f, lse = 0.f;
+        int tok = 0x7fffffff;
+        bool ovf = false;
+        if (folder) {
+            const int nh = G == 4 ? 1 : 2;
+            float mh = -1.0e30f, sh = 0.f;
+            for (int q = 0; q < p.S; ++q)
+                for (int f = 0; f < nh; ++f) {
+                    const float* pb = part_ptr(p, c.wg, q, c.wave + f) + c.lane;
+                    const float mk = pb[0], sk = pb[64];
+                    const float mn = fmaxf(mh, mk);
+                    sh = sh * __builtin_amdgcn_exp2f((mh - mn) * LOG2E) + sk * __builtin_amdgcn_exp2f((mk - mn) * LOG2E);
+                    mh = mn;
+                }
+            const float m_o = __shfl_xor(mh, 32);
+            const float s_o = __shfl_xor(sh, 32);
+            m = fmaxf(mh, m_o);
+            const float stot = sh * __builtin_amdgcn_exp2f((mh - m) * LOG2E) + s_o * __builtin_amdgcn_exp2f((m_o - m) * LOG2E);
+            lse = logf(stot);
+            for (int q = 0; q < p.S; ++q)
+                for (int f = 0; f < nh; ++f) {
+                    const float* pb = part_ptr(p, c.wg, q, c.wave + f) + c.lane;
+                    const float r0v = pb[128], r1v = pb[256], ev = pb[384];
+                    const int r0i = __builtin_bit_cast(int, pb[192]), r1i = __builtin_bit_cast(int, pb[320]);
+                    if (in_window(r0v, m, lse) && r0i < tok) tok = r0i;
+                    if (in_window(r1v, m, lse) && r1i < tok) tok = r1i;
+                    ovf = ovf || in_window(ev, m, lse);
+                }
+            tok = min(tok, __shfl_xor(tok, 32));
+            ovf = ovf || (__shfl_xor(ovf ? 1 : 0, 32) != 0);
+        }
+        if (__syncthreads_or((p.force_exact || ovf) ? 1 : 0)) {
+            // rare: more records than tracked fall in the tie window -> exact second pass over the
+            // whole vocabulary (every workgroup of the member does it: it needs the token)
+            const int nvt = (p.V1 + 31) >> 5;
+            auto desc = [&](int n) {
+                TileDesc d;
+                d.w_off = (uint32_t)p.off_log_w; d.ld = 128; d.row0 = 32 * n; d.nvalid = min(32, p.V1 - 32 * n); d.k0 = 0;
+                d.b_off = (uint32_t)p.off_log_b; d.pad_bias = NEG_INF;
+                return d;
+            };
+            StageRegs sr;
+            int best = 0x7fffffff;
+            stage_load(c.theta_r, c.noise_r, desc(0), c.tid, sr);
+            stage_store(lds, desc(0), c.sigma, c.tid, sr);
+            __syncthreads();
+            for (int n = 0; n < nvt; ++n) {
+                if (n + 1 < nvt) stage_load(c.theta_r, c.noise_r, desc(n + 1), c.tid, sr);
+                const float* buf = lds + (n & 1) * STAGE_FLOATS;
+                if (folder) {
+                    const f32x16 acc = mfma_tile(bias_init(buf + 2 * SIGN_FLOATS + 32 * c.sgn, c.hh), buf + c.sgn * SIGN_FLOATS, hB, c.lane);
+                    logit_epilogue_exact(best, acc, 32 * n + 4 * c.hh, m, lse);
+                }
+                if (n + 1 < nvt) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), c.sigma, c.tid, sr);
+                __syncthreads();
+            }
+            tok = min(best, __shfl_xor(best, 32));
+            if (lead) atomicAdd(p.stats + 0, 1);
+        }
+        if (tok >= p.V1) tok = 0;               // every logit NaN: end the caption (fused kernel rule)
+        const size_t o = (((size_t)c.member * 2 + c.sgn) * p.B + c.bc) * p.T + (t - 1);
+        const bool prev_unf = t == 1 || p.seq[o - 1] != 0;
+        const bool unfinished = prev_unf && tok > 0;
+        it = unfinished ? tok : 0;
+        if (c.q == 0 && folder && c.hh == 0 && c.row_valid) {
+            p.seq[o] = it;
+            if (p.lp) p.lp[o] = -lse;           // seq_logprobs[:, t-1] (nets.py:208,241)
+        }
+        const int any = __syncthreads_or((folder && unfinished && c.row_valid) ? 1 : 0);
+        if (lead) p.alive2[(t & 1) * p.alive_stride + c.wg] = any;
+        if (!any) return;                       // the reference stops here (nets.py:242-243)
+    } else if (t == 0) {
+        if (lead) p.alive2[c.wg] = 1;           // parity slot 0 read by step 1
+    }
+    if (t >= p.T) return;
+
+    // ---- LSTM cell of step t+1, gate tiles of this workgroup's unit blocks -------------------
+    float xB[64];
+    if (!folder) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) xB[i] = 0.f;
+    } else if (t < 0) {                                          // x = img_embed(fc) (nets.py:194-195)
+#pragma unroll
+        for (int i = 0; i < 64; ++i) xB[i] = ld1(c.scr_r, lo, X_SLOT(i));
+    } else {                                                     // x = embed(it) (nets.py:196-199)
+        const uint32_t eo = 4u * ((uint32_t)p.off_emb_w + (uint32_t)it * 128u + 4u * c.hh);
+#pragma unroll
+        for (int T = 0; T < 4; ++T)
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const f32x4 w = ld4(c.theta_r, eo + 4u * (32 * T + 8 * a));
+                const f32x4 z = ld4(c.noise_r, eo + 4u * (32 * T + 8 * a));
+                const f32x4 delta = c.sigma * z;
+                const f32x4 x = c.sgn ? (w - delta) : (w + delta);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) xB[16 * T + 4 * a + e] = x[e];
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) pin(xB[i]);
+    const uint32_t ib = (uint32_t)p.off_i2h_b, hb = (uint32_t)p.off_h2h_b, bmin = min(ib, hb);
+    auto csrc = [&](int m) {                                     // gate tile m: i2h rows | h2h rows
+        const uint32_t r = gate_row(m);
+        StageSrc Sx;
+        Sx.w_r = c.theta_r; Sx.z_r = c.noise_r; Sx.b_r = c.theta_r; Sx.bz_r = c.noise_r;
+        Sx.so_a = 4u * ((uint32_t)p.off_i2h_w + 128u * r);
+        Sx.so_b = 4u * ((uint32_t)p.off_h2h_w + 128u * r);
+        Sx.bso = 4u * (bmin + r);
+        Sx.bda = 4u * (ib - bmin); Sx.bdb = 4u * (hb - bmin);
+        Sx.valid = 64;
+        return Sx;
+    };
+    const int nb = 4 / (int)gridDim.x, m0 = 5 * nb * c.q, m1 = m0 + 5 * nb;
+    const int hpar = (t + 1) & 1;
+    Stage64Regs s64;
+    stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
+    stage64_store(lds, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
+    __syncthreads();
+    f32x16 hold;
+    auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) {
+        const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
+        const int U = m / 5, j5 = m % 5;
+        if (j5 == 0) {                                           // g1
+            hold = s_;
+        } else if (j5 == 1) {                                    // g = max(g1, g2)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hold[r] = hold[r] > s_[r] ? hold[r] : s_[r];
+        } else if (j5 == 2) {                                    // ig * g
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hold[r] = CELL_SIG(s_[r]) * hold[r];
+        } else if (j5 == 3) {                                    // c' = f * c + ig * g
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float fcv = CELL_SIG(s_[r]) * cpre[r];
+                const float cn = fcv + hold[r];
+                st1(c.scr_r, lo_, C_SLOT(16 * U + r), cn);
+                hold[r] = cn;
+            }
+        } else {                                                 // h' = o * tanh(c')
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                st1(c.scr_r, lo_, HP_SLOT(hpar, 16 * U + r), CELL_SIG(s_[r]) * CELL_TANH(hold[r]));
+        }
+    };
+    auto load_c = [&](int m) {                                   // c of the f tile's unit block
+        f32x16 cp;
+        const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cp[r] = (m % 5 == 3 && t >= 0) ? ld1(c.scr_r, lo_, C_SLOT(16 * (m / 5) + r)) : 0.f;
+        return cp;
+    };
+    float* xch = lds + 2 * STAGE64_FLOATS + (c.sgn * 2 + c.grp) * 1024;   // G = 2: h2h half -> i2h half
+#pragma unroll 1
+    for (int m = m0; m < m1; ++m) {
+        const f32x16 cpre = load_c(m);
+        __builtin_amdgcn_sched_barrier(0);
+        if (m + 1 < m1) stage64_load(csrc(m + 1), c.wave * 64 + lane_fresh(), s64);
+        const float* buf = lds + ((m - m0) & 1) * STAGE64_FLOATS;
+        if constexpr (G == 4) {
+            f32x16 a0, a1;
+            if (t < 0)      // h = 0 before the first cell: h2h(h) is its bias
+                mfma_xh_part<0, 4, false>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
+            else
+                mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
+            fold(m, a0 + a1, cpre);                              // i2h(x) + h2h(h), nets.py:109-111
+            if (m + 1 < m1) stage64_store(lds + ((m - m0 + 1) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
+            __syncthreads();
+        } else {
+            // half 0: i2h tile over x (chain a); half 1: h2h tile over h (chain b), handed over in LDS
+            const float* w1 = buf + c.sgn * (64 * LDS_ROW) + 32 * c.hf * LDS_ROW;
+            const float* b1 = buf + 2 * 64 * LDS_ROW + 64 * c.sgn + 32 * c.hf;
+            f32x16 a = bias_init(b1, lane_fresh() >> 5);
+            if (c.hf == 0) a = mfma_tile(a, w1, xB, lane_fresh());
+            else if (t >= 0) a = mfma_tile(a, w1, hB, lane_fresh());
+            if (c.hf == 1) {
+                const int l = lane_fresh();
+#pragma unroll
+                for (int r = 0; r < 16; ++r) xch[r * 64 + l] = a[r];
+            }
+            __syncthreads();
+            if (c.hf == 0) {
+                const int l = lane_fresh();
+                f32x16 a1;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) a1[r] = xch[r * 64 + l];
+                fold(m, a + a1, cpre);                           // i2h(x) + h2h(h), nets.py:109-111
+            }
+            if (m + 1 < m1) stage64_store(lds + ((m - m0 + 1) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
+            __syncthreads();
+        }
+    }
+}
+
+namespace {
+const size_t LDS64 = (size_t)(2 * STAGE64_FLOATS) * sizeof(float);
+const size_t LDS32 = (size_t)(2 * STAGE_FLOATS) * sizeof(float);
+const size_t LDS_CELL2 = LDS64 + (size_t)4 * 1024 * sizeof(float);   // + the G = 2 hand-over buffer
+}
+
+// per device, once per handle (nicnes_create, after hipSetDevice): dynamic LDS above 64 KB
+extern "C" hipError_t nicnes_decode_init() {
+    const struct { const void* f; size_t b; } ks[] = {
+        {(const void*)nicnes_decode_step_kernel, LDS64},
+        {(const void*)nicnes_decode_logit_kernel<4>, LDS64},
+        {(const void*)nicnes_decode_logit_kernel<2>, LDS64},
+        {(const void*)nicnes_decode_cell_kernel<4>, LDS64},
+        {(const void*)nicnes_decode_cell_kernel<2>, LDS_CELL2},
+        {(const void*)nicnes_decode_img_kernel<4>, LDS32},
+        {(const void*)nicnes_decode_img_kernel<2>, LDS32},
+    };
+    for (const auto& k : ks) {
+        hipError_t e = hipFuncSetAttribute(k.f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)k.b);
         if (e != hipSuccess) return e;
-        attr_set = true;
     }
-    if (evs && p->T + 4 > DECODE_MAX_EVENTS) return hipErrorInvalidValue;
+    return hipSuccess;
+}
+
+extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,
+                                           hipEvent_t* evs, int* kinds, int* n_launch) {
+    const bool fused = p->G == 4 && p->S == 1;
+    if (p->G != 4 && p->G != 2) return hipErrorInvalidValue;
+    if (p->S < 1 || p->S > 64) return hipErrorInvalidValue;
+    const int nl = fused ? p->T + 3 : 3 + 2 * p->T;
+    if (evs && nl + 1 > DECODE_MAX_EVENTS) return hipErrorInvalidValue;
     int ne = 0;
-    auto mark = [&]() { if (evs) (void)hipEventRecord(evs[ne++], stream); };
-    const dim3 grid(member_count, nslabs), block(NTHREADS);
-    mark();
-    hipLaunchKernelGGL(nicnes_decode_img_kernel, grid, block, lds32, stream, *p);
-    mark();
-    for (int t = -1; t <= p->T; ++t) {
-        hipLaunchKernelGGL(nicnes_decode_step_kernel, grid, block, lds64, stream, *p, t);
-        mark();
+    auto mark = [&](int kind) {
+        if (evs) {
+            if (ne > 0) kinds[ne] = kind;
+            (void)hipEventRecord(evs[ne++], stream);
+        }
+    };
+    const dim3 block(NTHREADS);
+    mark(0);
+    if (fused) {
+        hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(1, member_count, nslabs), block, LDS32, stream, *p);
+        mark(DK_IMG);
+        const dim3 grid(member_count, nslabs);
+        for (int t = -1; t <= p->T; ++t) {
+            hipLaunchKernelGGL(nicnes_decode_step_kernel, grid, block, LDS64, stream, *p, t);
+            mark(DK_STEP);
+        }
+    } else {
+        const int Sc = p->S < 4 ? p->S : 4;
+        const dim3 gl(p->S, member_count, nslabs), gc(Sc, member_count, nslabs);
+        if (p->G == 4) {
+            hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, gc, block, LDS32, stream, *p);
+            mark(DK_IMG);
+            for (int t = -1; t <= p->T; ++t) {
+                if (t >= 1) {
+                    hipLaunchKernelGGL(nicnes_decode_logit_kernel<4>, gl, block, LDS64, stream, *p, t);
+                    mark(DK_LOGIT);
+                }
+                hipLaunchKernelGGL(nicnes_decode_cell_kernel<4>, gc, block, LDS64, stream, *p, t);
+                mark(DK_CELL);
+            }
+        } else {
+            hipLaunchKernelGGL(nicnes_decode_img_kernel<2>, gc, block, LDS32, stream, *p);
+            mark(DK_IMG);
+            for (int t = -1; t <= p->T; ++t) {
+                if (t >= 1) {
+                    hipLaunchKernelGGL(nicnes_decode_logit_kernel<2>, gl, block, LDS64, stream, *p, t);
+                    mark(DK_LOGIT);
+                }
+                hipLaunchKernelGGL(nicnes_decode_cell_kernel<2>, gc, block, LDS_CELL2, stream, *p, t);
+                mark(DK_CELL);
+            }
+        }
     }
+    if (n_launch) *n_launch = ne;
     return hipGetLastError();
 }
 
-extern "C" size_t nicnes_decode_scratch_floats(int member_count, int nslabs) {
-    return (size_t)member_count * nslabs * 8 * SCR_SLOTS * 64;
+extern "C" size_t nicnes_decode_scratch_floats(int member_count, int row_waves_per_member) {
+    return (size_t)member_count * row_waves_per_member * SCR_SLOTS * 64;
 }

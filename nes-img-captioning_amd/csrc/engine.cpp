@@ -69,7 +69,12 @@ struct nicnes_handle {
     int fitness_mode = 0;             // nicnes_set_fitness_mode (0 = 'greedy')
     float* dscratch = nullptr;
     int32_t* stats = nullptr;
-    int32_t* alive = nullptr;         // per decode workgroup: rows left unfinished
+    int32_t* alive = nullptr;         // per decode workgroup: rows left unfinished (fused [stride], split [2][stride])
+    int32_t alive_stride = 0;         // max decode workgroups (members x 64-row slabs)
+    float* part = nullptr;            // split decode: partial greedy states
+    int64_t part_cap = 0;             // in logit workgroups (members x slabs x S)
+    int n_cu = 256;
+    int dec_S = 0, dec_G = 0;         // nicnes_set_decode_split (0 = automatic)
     double* partials = nullptr;
     double* norms = nullptr;
 
@@ -77,6 +82,7 @@ struct nicnes_handle {
     int force_exact = 0;      // test hook: exact tie pass on every step (NICNES_FORCE_EXACT=1)
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     hipEvent_t dev[DECODE_MAX_EVENTS] = {};   // between the decode's launches (phase split)
+    int dev_kind[DECODE_MAX_EVENTS] = {};     // kind of the launch each event follows (DK_*)
     int n_dev = 0;                            // events recorded by the last timed decode
 };
 
@@ -115,7 +121,37 @@ __global__ void f64_to_f32_kernel(const double* in, float* out, int64_t n) {
     if (i < n) out[i] = (float)in[i];
 }
 
-int nslabs_of(int B) { return (B + 127) / 128; }
+// decode shape: G row groups per slab (4: 128-row slabs; 2: 64-row slabs when that pads fewer rows,
+// e.g. mscoco_nes.json's batch_size 64), and S logit workgroups per member slab
+int auto_G(int B) { return (B + 63) / 64 * 64 < (B + 127) / 128 * 128 ? 2 : 4; }
+int nslabs_of(int B, int G) { return (B + 32 * G - 1) / (32 * G); }
+
+// S minimising the makespan ceil(n_wg * S / n_cu) * (1/S + per-workgroup overhead); the split path
+// (two launches per step) is charged 2 % over the fused step kernel
+int auto_split(int64_t n_wg, int n_cu, int G) {
+    int best = 1;
+    double bc = 1e300;
+    for (int S = 1; S <= 16; S *= 2) {
+        const double rounds = std::ceil((double)n_wg * S / n_cu);
+        const double cost = rounds * (1.0 / S + 0.03) * ((G == 4 && S > 1) ? 1.02 : 1.0);
+        if (cost < bc - 1e-12) {
+            bc = cost;
+            best = S;
+        }
+    }
+    return best;
+}
+
+// logit workgroups the automatic rule can ask for, up to max_members x the widest slab count
+int64_t auto_part_cap(int max_members, int max_batch, int n_cu) {
+    int64_t cap = 1;
+    for (int G = 2; G <= 4; G += 2) {
+        const int ns = nslabs_of(max_batch, G);
+        for (int64_t n = 1; n <= (int64_t)max_members * ns; ++n)
+            cap = std::max(cap, n * auto_split(n, n_cu, G));
+    }
+    return cap;
+}
 
 template <class T>
 int dalloc(nicnes_handle* h, T** p, size_t n) {
@@ -123,6 +159,12 @@ int dalloc(nicnes_handle* h, T** p, size_t n) {
     hipError_t e = hipMalloc((void**)p, n * sizeof(T));
     if (e != hipSuccess) return fail(h, NICNES_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
     return NICNES_OK;
+}
+
+void decode_shape(const nicnes_handle* h, int B, int count, int* G, int* nslabs, int* S) {
+    *G = h->dec_G ? h->dec_G : auto_G(B);
+    *nslabs = nslabs_of(B, *G);
+    *S = h->dec_S ? h->dec_S : auto_split((int64_t)count * *nslabs, h->n_cu, *G);
 }
 
 }  // namespace
@@ -193,9 +235,20 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
         const char* fe = getenv("NICNES_FORCE_EXACT");
         h->force_exact = (fe && fe[0] == '1') ? 1 : 0;
     }
-    if (!rc) rc = dalloc(h, &h->dscratch, nicnes_decode_scratch_floats((int)MM, nslabs_of((int)MB)));
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+            h->n_cu = ncu;
+    }
+    if (!rc && nicnes_decode_init() != hipSuccess) rc = fail(h, NICNES_ERR_HIP, "nicnes_decode_init");
+    // lane scratch: 2G row waves per slab, the larger of the two slab layouts
+    const int rw = std::max(8 * nslabs_of((int)MB, 4), 4 * nslabs_of((int)MB, 2));
+    h->alive_stride = (int32_t)(MM * (size_t)nslabs_of((int)MB, 2));
+    h->part_cap = auto_part_cap((int)MM, (int)MB, h->n_cu);
+    if (!rc) rc = dalloc(h, &h->dscratch, nicnes_decode_scratch_floats((int)MM, rw));
     if (!rc) rc = dalloc(h, &h->stats, 4);
-    if (!rc) rc = dalloc(h, &h->alive, MM * (size_t)nslabs_of((int)MB));
+    if (!rc) rc = dalloc(h, &h->alive, 3 * (size_t)h->alive_stride);
+    if (!rc) rc = dalloc(h, &h->part, (size_t)h->part_cap * PART_FLOATS);
     if (!rc) rc = dalloc(h, &h->partials, 2 * (size_t)nicnes_adam_blocks(h->D));
     if (!rc) rc = dalloc(h, &h->norms, 2);
     if (rc) {
@@ -218,7 +271,7 @@ int nicnes_destroy(nicnes_handle* h) {
     (void)hipSetDevice(h->device);
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
                     h->ref_norm, h->nidx, h->seq, h->lp, h->row_scores, h->dscratch, h->stats, h->partials, h->norms,
-                    h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive};
+                    h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive, h->part};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : h->ev)
@@ -415,6 +468,15 @@ int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begi
     p.alive = h->alive;
     p.sigma = sigma;
     p.force_exact = h->force_exact;
+    int G = 0, nslabs = 0, S = 0;
+    decode_shape(h, h->B, count, &G, &nslabs, &S);
+    if ((int64_t)count * nslabs * S > h->part_cap)
+        return fail(h, NICNES_ERR_INVALID, "decode split beyond the partial-state buffer (nicnes_set_decode_split)");
+    p.G = G;
+    p.S = S;
+    p.part = h->part;
+    p.alive2 = h->alive + h->alive_stride;
+    p.alive_stride = h->alive_stride;
     p.B = h->B;
     p.F = h->cfg.fc_feat_size;
     p.V1 = h->V1;
@@ -433,8 +495,9 @@ int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begi
     HIPC(h, hipMemsetAsync(p.seq, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(int32_t), s));
     if (p.lp) HIPC(h, hipMemsetAsync(p.lp, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(float), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
-    HIPC(h, nicnes_launch_decode(&p, count, nslabs_of(h->B), s, h->timing ? h->dev : nullptr));
-    h->n_dev = h->timing ? p.T + 4 : 0;
+    int n_ev = 0;
+    HIPC(h, nicnes_launch_decode(&p, count, nslabs, s, h->timing ? h->dev : nullptr, h->dev_kind, &n_ev));
+    h->n_dev = h->timing ? n_ev : 0;
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     CiderTables tb = tables_of(h);
     if (h->img_tables)
@@ -573,23 +636,61 @@ int nicnes_kernel_times(nicnes_handle* h, float* out2_host) {
     return NICNES_OK;
 }
 
-int nicnes_decode_phase_times(nicnes_handle* h, float* out4_host) {
-    if (!h || !out4_host || h->n_dev < 5) return NICNES_ERR_INVALID;
+int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host) {
+    if (!h || !out8_host || h->n_dev < 3) return NICNES_ERR_INVALID;
     HIPC(h, hipSetDevice(h->device));
     HIPC(h, hipEventSynchronize(h->dev[h->n_dev - 1]));
-    // event k follows launch k: img, then step(t) for t = -1..T. Steps -1 and 0 run only a cell
-    // (no logits); every later step runs logits + token, then the next cell.
-    float img = 0.f, cell_only = 0.f, step = 0.f, ms = 0.f;
+    // event k follows launch k. Fused: img, then step(t) for t = -1..T (the first two launches run
+    // only a cell). Split: img, cell(-1), cell(0), then logit(t), cell(t) for t = 1..T.
+    float o[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ms = 0.f;
+    int n_cell_only = 0;
     for (int k = 1; k < h->n_dev; ++k) {
         HIPC(h, hipEventElapsedTime(&ms, h->dev[k - 1], h->dev[k]));
-        if (k == 1) img += ms;
-        else step += ms;
-        if (k == 2 || k == 3) cell_only += ms;
+        switch (h->dev_kind[k]) {
+            case DK_IMG: o[0] += ms; break;
+            case DK_STEP:
+                o[2] += ms; o[3] += 1;
+                if (n_cell_only < 2) { o[1] += ms; ++n_cell_only; }
+                break;
+            case DK_LOGIT: o[4] += ms; o[5] += 1; break;
+            default:
+                o[6] += ms; o[7] += 1;
+                if (n_cell_only < 2) { o[1] += ms; ++n_cell_only; }
+                break;
+        }
     }
-    out4_host[0] = img;
-    out4_host[1] = cell_only;
-    out4_host[2] = step;
-    out4_host[3] = (float)(h->n_dev - 2);
+    for (int i = 0; i < 8; ++i) out8_host[i] = o[i];
+    return NICNES_OK;
+}
+
+int nicnes_set_decode_split(nicnes_handle* h, int32_t S, int32_t G) {
+    if (!h || S < 0 || S > 64 || (G != 0 && G != 2 && G != 4)) return NICNES_ERR_INVALID;
+    HIPC(h, hipSetDevice(h->device));
+    if (S > 0) {
+        const int ns = std::max(nslabs_of(h->cfg.max_batch, 2), nslabs_of(h->cfg.max_batch, 4));
+        const int64_t need = (int64_t)h->cfg.max_members * ns * S;
+        if (need > h->part_cap) {
+            float* np = nullptr;
+            int rc = dalloc(h, &np, (size_t)need * PART_FLOATS);
+            if (rc) return rc;
+            HIPC(h, hipDeviceSynchronize());
+            (void)hipFree(h->part);
+            h->part = np;
+            h->part_cap = need;
+        }
+    }
+    h->dec_S = S;
+    h->dec_G = G;
+    return NICNES_OK;
+}
+
+int nicnes_decode_shape(nicnes_handle* h, int32_t B, int32_t count, int32_t* out3_host) {
+    if (!h || !out3_host || B < 1 || count < 1) return NICNES_ERR_INVALID;
+    int G, ns, S;
+    decode_shape(h, B, count, &G, &ns, &S);
+    out3_host[0] = G;
+    out3_host[1] = ns;
+    out3_host[2] = S;
     return NICNES_OK;
 }
 

@@ -15,7 +15,8 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_get_adam_state', 'nicnes_set_batch', 'nicnes_set_df_table', 'nicnes_noise_indices',
            'nicnes_evaluate', 'nicnes_rank_weights', 'nicnes_grad_partial', 'nicnes_adam_step', 'nicnes_stats',
            'nicnes_set_timing', 'nicnes_kernel_times', 'nicnes_decode_phase_times', 'nicnes_sgd_step',
-           'nicnes_optimizer_update', 'nicnes_last_ratio', 'nicnes_set_fitness_mode', 'nicnes_evaluate_lp']
+           'nicnes_optimizer_update', 'nicnes_last_ratio', 'nicnes_set_fitness_mode', 'nicnes_evaluate_lp',
+           'nicnes_set_decode_split', 'nicnes_decode_shape']
 
 
 class NicnesConfig(ctypes.Structure):
@@ -68,6 +69,8 @@ def lib(path=None):
         'nicnes_set_timing': (c.c_int, [vp, c.c_int]),
         'nicnes_kernel_times': (c.c_int, [vp, vp]),
         'nicnes_decode_phase_times': (c.c_int, [vp, vp]),
+        'nicnes_set_decode_split': (c.c_int, [vp, i32, i32]),
+        'nicnes_decode_shape': (c.c_int, [vp, i32, i32, vp]),
         'nicnes_last_ratio': (c.c_int, [vp, vp, vp]),
         'nicnes_sgd_step': (c.c_int, [vp, vp, i32, f64, f64, f64, vp, vp]),
         'nicnes_optimizer_update': (c.c_int, [vp, c.c_int, vp, c.c_int, f64, f64, f64, f64, vp, vp]),

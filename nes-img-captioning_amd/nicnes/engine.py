@@ -57,6 +57,7 @@ class Engine:
         with torch.cuda.device(self.device):
             check(self.L.nicnes_create(ctypes.byref(self.cfg), device, ctypes.byref(h)), None, 'nicnes_create')
         self.h = h
+        self.n_cu = torch.cuda.get_device_properties(self.device).multi_processor_count
         self._keep = {}
         self.B = 0
 
@@ -246,13 +247,25 @@ class Engine:
         return float(out[0]), float(out[1])
 
     def decode_phase_times(self):
-        """Per-kernel split of the last timed decode: {'img_ms', 'cell_only_ms', 'step_ms',
-        'step_launches'} (step_ms sums the T+2 step-kernel launches, cell_only_ms its two launches
-        without logits, t = -1 and 0; HIP events between the launches)."""
-        out = (ctypes.c_float * 4)()
+        """Per-kernel split of the last timed decode (HIP events between its launches): img_ms,
+        cell_only_ms (the t = -1, 0 launches), step_ms / step_launches (fused step kernel, t = -1..T),
+        logit_ms / logit_launches and cell_ms / cell_launches (split path)."""
+        out = (ctypes.c_float * 8)()
         check(self.L.nicnes_decode_phase_times(self.h, out), self.h, 'decode_phase_times')
         return {'img_ms': float(out[0]), 'cell_only_ms': float(out[1]), 'step_ms': float(out[2]),
-                'step_launches': int(out[3])}
+                'step_launches': int(out[3]), 'logit_ms': float(out[4]), 'logit_launches': int(out[5]),
+                'cell_ms': float(out[6]), 'cell_launches': int(out[7])}
+
+    def set_decode_split(self, S=0, G=0):
+        """Force the decode shape (S logit workgroups per member slab, G = 4 / 2 row groups per slab);
+        0 = automatic. Tokens do not depend on it."""
+        check(self.L.nicnes_set_decode_split(self.h, int(S), int(G)), self.h, 'set_decode_split')
+
+    def decode_shape(self, B=None, count=1):
+        """(G, slabs, S) an evaluate of `count` members would use."""
+        out = (ctypes.c_int32 * 3)()
+        check(self.L.nicnes_decode_shape(self.h, int(B or self.B), int(count), out), self.h, 'decode_shape')
+        return tuple(int(v) for v in out)
 
     def stats(self):
         out = (ctypes.c_int64 * 4)()
