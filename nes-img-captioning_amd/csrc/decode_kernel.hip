@@ -235,18 +235,70 @@ __device__ __forceinline__ void stage64_load(const StageSrc& S, int tid, Stage64
 }
 
 __device__ __forceinline__ void stage64_store(float* buf, int valid, float sigma, int tid, const Stage64Regs& r) {
+    // thread tid writes rows (tid >> 5) + 16u: one base offset, the row step rides in the ds offset
+    const int q = tid & 31;
+    float* b = buf + (tid >> 5) * LDS_ROW + (q >> 3) * 32 + (q & 1) * 16 + 4 * ((q & 7) >> 1);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const int f = tid + NTHREADS * u, row = f >> 5, q = f & 31;
-        const int o = row * LDS_ROW + (q >> 3) * 32 + (q & 1) * 16 + 4 * ((q & 7) >> 1);
         const f32x4 delta = sigma * r.z[u];           // fp32(sigma * z), nets.py:102
-        *reinterpret_cast<f32x4*>(buf + o) = r.w[u] + delta;                    // nets.py:113
-        *reinterpret_cast<f32x4*>(buf + 64 * LDS_ROW + o) = r.w[u] - delta;     // nic_nes_worker.py:151
+        *reinterpret_cast<f32x4*>(b + 16 * u * LDS_ROW) = r.w[u] + delta;                  // nets.py:113
+        *reinterpret_cast<f32x4*>(b + (64 + 16 * u) * LDS_ROW) = r.w[u] - delta;           // nic_nes_worker.py:151
     }
     const int row = tid & 63, sg = (tid >> 6) & 1;     // every pair of waves writes all 128 slots
     const float delta = sigma * r.bz;
     const float v = sg ? r.bw - delta : r.bw + delta;
     buf[2 * 64 * LDS_ROW + 64 * sg + row] = row < valid ? v : NEG_INF;
+}
+
+// Per-lane offsets of the logit stage loop, computed once per kernel (the loop would otherwise
+// recompute them from the lane id at every stage): global load byte offset, LDS store float offset,
+// MFMA A-operand row float offset, bias slot.
+struct LaneOffs {
+    uint32_t vo;      // 16 * tid: row (tid >> 5) + 16u, k 4 * (tid & 31) of a 32-row tile
+    uint32_t vb;      // bias: 4 * (lane & 31) + tile-b byte offset for lanes 32..63
+    int so;           // LDS float offset of this thread's first staged f32x4
+    int arow;         // A-operand row of this lane: (lane & 31) * LDS_ROW + 16 * (lane >> 5)
+    int bslot;        // bias slot: 64 * sign + row
+};
+
+__device__ __forceinline__ LaneOffs lane_offs(int wave, uint32_t bdb) {
+    LaneOffs o;
+    const int lane = lane_fresh(), tid = wave * 64 + lane, q = tid & 31;
+    o.vo = 16u * (uint32_t)tid;
+    o.vb = 4u * (uint32_t)(lane & 31) + ((lane & 32) ? bdb : 0u);
+    o.so = (tid >> 5) * LDS_ROW + (q >> 3) * 32 + (q & 1) * 16 + 4 * ((q & 7) >> 1);
+    o.arow = (lane & 31) * LDS_ROW + 16 * (lane >> 5);
+    o.bslot = 64 * ((tid >> 6) & 1) + (tid & 63);
+    return o;
+}
+
+__device__ __forceinline__ void stage64_load_o(const StageSrc& S, const LaneOffs& o, bool bias, Stage64Regs& r) {
+    if (bias) {                                       // waves 0 and 1 stage the 2 x 64 bias slots
+        r.bw = ld1(S.b_r, o.vb, S.bso);
+        r.bz = ld1(S.bz_r, o.vb, S.bso);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t so = (u < 2 ? S.so_a : S.so_b) + 8192u * (uint32_t)(u & 1);
+        r.w[u] = ld4(S.w_r, o.vo, so);
+        r.z[u] = ld4(S.z_r, o.vo, so);
+    }
+}
+
+__device__ __forceinline__ void stage64_store_o(float* buf, int valid, float sigma, const LaneOffs& o, bool bias,
+                                                const Stage64Regs& r) {
+    float* b = buf + o.so;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const f32x4 delta = sigma * r.z[u];           // fp32(sigma * z), nets.py:102
+        *reinterpret_cast<f32x4*>(b + 16 * u * LDS_ROW) = r.w[u] + delta;                  // nets.py:113
+        *reinterpret_cast<f32x4*>(b + (64 + 16 * u) * LDS_ROW) = r.w[u] - delta;           // nic_nes_worker.py:151
+    }
+    if (bias) {
+        const float delta = sigma * r.bz;
+        const float v = o.bslot >= 64 ? r.bw - delta : r.bw + delta;
+        buf[2 * 64 * LDS_ROW + o.bslot] = (o.bslot & 63) < valid ? v : NEG_INF;
+    }
 }
 
 // two independent accumulator chains (stage rows 0-31 and 32-63) over the same B
@@ -271,6 +323,42 @@ __device__ __forceinline__ void mfma_stage64(const float* w, const float* bias, 
             acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
         }
     }
+}
+
+__device__ __forceinline__ void mfma_stage64_o(const float* w, const float* bias, const float (&Bop)[64], int arow,
+                                               int hh, f32x16& acc0, f32x16& acc1) {
+    const float* row0 = w + arow;
+    const float* row1 = row0 + 32 * LDS_ROW;
+    acc0 = bias_init(bias, hh);
+    acc1 = bias_init(bias + 32, hh);
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+        f32x4 a0[4], a1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            a0[c] = *reinterpret_cast<const f32x4*>(row0 + T * 32 + 4 * c);
+            a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bop[16 * T + jj], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
+        }
+    }
+}
+
+__device__ __forceinline__ f32x16 mfma_tile_o(f32x16 acc, const float* w, const float (&Bop)[64], int arow) {
+    const float* row = w + arow;
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+        f32x4 a[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] = *reinterpret_cast<const f32x4*>(row + T * 32 + 4 * c);
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[jj >> 2][jj & 3], Bop[16 * T + jj], acc, 0, 0, 0);
+    }
+    return acc;
 }
 
 // cell stage: chain a = i2h tile (stage rows 0-31) over B = x, chain b = h2h tile (rows 32-63)
@@ -341,33 +429,58 @@ __device__ __forceinline__ float max4(const f32x16& P, int k) {
     return fmaxf(fmaxf(fmaxf(P[4 * k], P[4 * k + 1]), P[4 * k + 2]), P[4 * k + 3]);
 }
 
+// v_max3 / v_max without the quieting copies LLVM puts in front of fmaxf on values it cannot prove
+// canonical (every MFMA result): logits are NaN-free except in the all-NaN edge case, where the
+// greedy rule ends the caption anyway (tok >= V1 -> 0)
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float vmax2(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// maximum of 15 + 1 values: 5 + 2 v_max3
+__device__ __forceinline__ float vmax16(const f32x16& A) {
+    const float a0 = vmax3(A[0], A[1], A[2]), a1 = vmax3(A[3], A[4], A[5]), a2 = vmax3(A[6], A[7], A[8]);
+    const float a3 = vmax3(A[9], A[10], A[11]), a4 = vmax3(A[12], A[13], A[14]);
+    return vmax3(vmax3(a0, a1, a2), a3, vmax2(a4, A[15]));
+}
+
+// record scans of one stage, run only in the (wave-uniform) case that some lane sees a new running
+// max in it: per group of 4 consecutive vocab ids, again only where a lane's group max is a record
+__device__ __forceinline__ void records_scan(RowState& st, const f32x16& P, int vbase) {
+    const float g0 = max4(P, 0), g1 = max4(P, 1), g2 = max4(P, 2), g3 = max4(P, 3);
+    if (__any(g0 > st.r1v)) records4<0>(st, P, vbase);
+    if (__any(g1 > st.r1v)) records4<1>(st, P, vbase);
+    if (__any(g2 > st.r1v)) records4<2>(st, P, vbase);
+    if (__any(g3 > st.r1v)) records4<3>(st, P, vbase);
+}
+
+// online exp-sum: s = s * e^(m - mnew) + sum_r e^(P[r] - mnew), in vocab order
+__device__ __forceinline__ void expsum16(float& s, const f32x16& P, float ml) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(P[r], LOG2E, -ml));
+}
+
 // epilogue of one logit stage: P0 holds vocab vbase + (r&3) + 8(r>>2), P1 the same + 32.
-// Record scans run per group of 4 consecutive vocab ids, only in the (wave-uniform) case that
-// some lane sees a new running max in that group: a wave covers 32 rows, so whole-stage scans
-// would run in most stages, while a group scan is needed in few once the running max settles.
+// Per stage and lane: 15 v_max3/v_max for the stage max, then 3 VALU per logit for the exp-sum; the
+// record scans run only in stages that raise some lane's running max (few once it settles).
 __device__ __forceinline__ void epilogue64(RowState& st, const f32x16& P0, const f32x16& P1, int vbase) {
-    const float g0 = max4(P0, 0), g1 = max4(P0, 1), g2 = max4(P0, 2), g3 = max4(P0, 3);
-    const float g4 = max4(P1, 0), g5 = max4(P1, 1), g6 = max4(P1, 2), g7 = max4(P1, 3);
-    const float tmax = fmaxf(fmaxf(fmaxf(g0, g1), fmaxf(g2, g3)), fmaxf(fmaxf(g4, g5), fmaxf(g6, g7)));
-    const float mnew = fmaxf(st.m, tmax);
+    const float tmax = vmax2(vmax16(P0), vmax16(P1));
+    if (__any(tmax > st.r1v)) {
+        records_scan(st, P0, vbase);
+        records_scan(st, P1, vbase + 32);
+    }
+    const float mnew = vmax2(st.m, tmax);
     const float ml = mnew * LOG2E;
     float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(P0[r], LOG2E, -ml));
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(P1[r], LOG2E, -ml));
+    expsum16(s, P0, ml);
+    expsum16(s, P1, ml);
     st.s = s;
     st.m = mnew;
-    if (__any(tmax > st.r1v)) {
-        if (__any(g0 > st.r1v)) records4<0>(st, P0, vbase);
-        if (__any(g1 > st.r1v)) records4<1>(st, P0, vbase);
-        if (__any(g2 > st.r1v)) records4<2>(st, P0, vbase);
-        if (__any(g3 > st.r1v)) records4<3>(st, P0, vbase);
-        if (__any(g4 > st.r1v)) records4<0>(st, P1, vbase + 32);
-        if (__any(g5 > st.r1v)) records4<1>(st, P1, vbase + 32);
-        if (__any(g6 > st.r1v)) records4<2>(st, P1, vbase + 32);
-        if (__any(g7 > st.r1v)) records4<3>(st, P1, vbase + 32);
-    }
 }
 
 // exact mode (fallback): first v with fp32((L - m) - lse) == -lse
@@ -381,6 +494,104 @@ __device__ __forceinline__ void logit_epilogue_exact(int& best, const f32x16& ac
 }
 
 __device__ __forceinline__ bool in_window(float v, float m, float lse) { return ((v - m) - lse) == -lse; }
+
+// epilogue of one 32-row logit tile (G = 2: one tile per wave); P0 holds vocab vbase + (r&3) + 8(r>>2)
+__device__ __forceinline__ void epilogue32(RowState& st, const f32x16& P0, int vbase) {
+    const float tmax = vmax16(P0);
+    if (__any(tmax > st.r1v)) records_scan(st, P0, vbase);
+    const float mnew = vmax2(st.m, tmax);
+    const float ml = mnew * LOG2E;
+    float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
+    expsum16(s, P0, ml);
+    st.s = s;
+    st.m = mnew;
+}
+
+// The logit GEMM of one step over 64-row stages [s0, s1) of the vocabulary, double-buffered in LDS
+// from `lds` (stage s0 in buffer 0); the greedy state of this lane's rows accumulates in st.
+// G = 4: each wave runs both 32-row tiles of a stage (two MFMA chains); G = 2: tile hf only.
+// Stages alternate between two accumulator sets, so no stage copies its result for the next one's
+// epilogue; the two waves of a SIMD (w, w + 4: opposite signs) run MFMA and epilogue in opposite
+// orders. On return the last stage_store went to buffer (s1 - s0) & 1 (a redundant copy).
+template <int G>
+__device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, uint64_t nidx, int wave, int sgn,
+                                             int hf, float sigma, const float (&hB)[64], int s0, int s1, RowState& st) {
+    const rsrc_t lw_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
+    const rsrc_t lz_r = make_rsrc(p.noise + nidx + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
+    const rsrc_t lbw_r = make_rsrc(p.theta + p.off_log_b, 4u * (uint32_t)p.V1);
+    const rsrc_t lbz_r = make_rsrc(p.noise + nidx + p.off_log_b, 4u * (uint32_t)p.V1);
+    auto lsrc = [&](int s) {                                 // logit rows 64s .. 64s+63
+        StageSrc Sx;
+        Sx.w_r = lw_r; Sx.z_r = lz_r; Sx.b_r = lbw_r; Sx.bz_r = lbz_r;
+        Sx.so_a = 32768u * (uint32_t)s; Sx.so_b = Sx.so_a + 16384u;
+        Sx.bso = 256u * (uint32_t)s; Sx.bda = 0u; Sx.bdb = 128u;
+        Sx.valid = p.V1 - 64 * s;
+        return Sx;
+    };
+    const LaneOffs lo = lane_offs(wave, 128u);
+    const int hh = lane_fresh() >> 5, vl = 4 * hh + (G == 4 ? 0 : 32 * hf);
+    const bool bias = wave < 2;
+    Stage64Regs s64;
+    stage64_load_o(lsrc(s0), lo, bias, s64);
+    stage64_store_o(lds, lsrc(s0).valid, sigma, lo, bias, s64);
+    __syncthreads();
+    f32x16 a0, a1, b0, b1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { b0[r] = NEG_INF; b1[r] = NEG_INF; }
+    auto stage = [&](int s, f32x16& o0, f32x16& o1, const f32x16& q0, const f32x16& q1) {
+        const int sn = min(s + 1, s1 - 1);
+#if !(DECODE_ABLATE & 2)
+        stage64_load_o(lsrc(sn), lo, bias, s64);
+#endif
+        const float* buf = lds + ((s - s0) & 1) * STAGE64_FLOATS;
+        const float* wsg = buf + sgn * (64 * LDS_ROW);
+        const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * sgn;
+        if constexpr (G == 4) {
+            if (sgn == 0) {
+                mfma_stage64_o(wsg, bsg, hB, lo.arow, hh, o0, o1);
+#if !(DECODE_ABLATE & 1)
+                epilogue64(st, q0, q1, 64 * (s - 1) + vl);
+#endif
+            } else {
+#if !(DECODE_ABLATE & 1)
+                epilogue64(st, q0, q1, 64 * (s - 1) + vl);
+#endif
+                mfma_stage64_o(wsg, bsg, hB, lo.arow, hh, o0, o1);
+            }
+        } else {
+            const float* w1 = wsg + 32 * hf * LDS_ROW;         // this wave's 32-row tile of the stage
+            const float* bb = bsg + 32 * hf;
+            if (sgn == 0) {
+                o0 = mfma_tile_o(bias_init(bb, hh), w1, hB, lo.arow);
+                epilogue32(st, q0, 64 * (s - 1) + vl);
+            } else {
+                epilogue32(st, q0, 64 * (s - 1) + vl);
+                o0 = mfma_tile_o(bias_init(bb, hh), w1, hB, lo.arow);
+            }
+        }
+#if !(DECODE_ABLATE & 2)
+        stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, sigma, lo, bias, s64);
+#endif
+#if !(DECODE_ABLATE & 8)
+        __syncthreads();
+#endif
+    };
+    auto last = [&](const f32x16& q0, const f32x16& q1, int s) {
+        if constexpr (G == 4)
+            epilogue64(st, q0, q1, 64 * s + vl);
+        else
+            epilogue32(st, q0, 64 * s + vl);
+    };
+    for (int s = s0; s < s1; s += 2) {
+        stage(s, a0, a1, b0, b1);
+        if (s + 1 == s1) {
+            last(a0, a1, s);
+            return;
+        }
+        stage(s + 1, b0, b1, a0, a1);
+    }
+    last(b0, b1, s1 - 1);
+}
 
 // gate tiles of the cell: tile m = 0..19 is gate chunk tile_q(m) (order g1, g2, i, f, o) of the
 // 32-unit block U = m / 5; its 32 rows of the 640-row i2h / h2h matrices start at gate_row(m)
@@ -555,56 +766,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
     Stage64Regs s64;
     int it = 0;                                   // token fed to the next cell (0 = BOS at t = 0)
     if (nl > 0) {
-        const rsrc_t lw_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
-        const rsrc_t lz_r = make_rsrc(p.noise + nidx + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
-        const rsrc_t lbw_r = make_rsrc(p.theta + p.off_log_b, 4u * (uint32_t)p.V1);
-        const rsrc_t lbz_r = make_rsrc(p.noise + nidx + p.off_log_b, 4u * (uint32_t)p.V1);
-        auto lsrc = [&](int s) {                                 // logit rows 64s .. 64s+63
-            StageSrc S;
-            S.w_r = lw_r; S.z_r = lz_r; S.b_r = lbw_r; S.bz_r = lbz_r;
-            S.so_a = 32768u * (uint32_t)s; S.so_b = S.so_a + 16384u;
-            S.bso = 256u * (uint32_t)s; S.bda = 0u; S.bdb = 128u;
-            S.valid = p.V1 - 64 * s;
-            return S;
-        };
         RowState st;
         row_state_init(st);
-        stage64_load(lsrc(0), c.wave * 64 + lane_fresh(), s64);
-        stage64_store(lds, lsrc(0).valid, c.sigma, c.wave * 64 + lane_fresh(), s64);
-        __syncthreads();
-        f32x16 prev0, prev1;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { prev0[r] = NEG_INF; prev1[r] = NEG_INF; }
-        for (int s = 0; s < nl; ++s) {
-            const int sn = min(s + 1, nl - 1);
-#if !(DECODE_ABLATE & 2)
-            stage64_load(lsrc(sn), c.wave * 64 + lane_fresh(), s64);
-#endif
-            const float* buf = lds + (s & 1) * STAGE64_FLOATS;
-            const float* wsg = buf + c.sgn * (64 * LDS_ROW);
-            const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * c.sgn;
-            f32x16 acc0, acc1;
-            if (c.sgn == 0) {
-                mfma_stage64(wsg, bsg, hB, lane_fresh(), acc0, acc1);
-#if !(DECODE_ABLATE & 1)
-                epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
-#endif
-            } else {
-#if !(DECODE_ABLATE & 1)
-                epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
-#endif
-                mfma_stage64(wsg, bsg, hB, lane_fresh(), acc0, acc1);
-            }
-#if !(DECODE_ABLATE & 2)
-            stage64_store(lds + ((s + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, c.sigma, c.wave * 64 + lane_fresh(), s64);
-#endif
-#if !(DECODE_ABLATE & 8)
-            __syncthreads();
-#endif
-            prev0 = acc0;
-            prev1 = acc1;
-        }
-        epilogue64(st, prev0, prev1, 64 * (nl - 1) + 4 * (lane_fresh() >> 5));
+        logit_stages<4>(lds, p, nidx, c.wave, c.sgn, 0, c.sigma, hB, 0, nl, st);
 
         // ---- greedy token (nets.py:208-209) ------------------------------------------------
         const float m_o = __shfl_xor(st.m, 32);
@@ -777,25 +941,6 @@ __device__ __forceinline__ float* part_ptr(const DecodeParams& p, int wg, int q,
     return p.part + (((size_t)wg * p.S + q) * 8 + wave) * (7 * 64);
 }
 
-// epilogue of one 32-row logit tile (G = 2: one tile per wave); P0 holds vocab vbase + (r&3) + 8(r>>2)
-__device__ __forceinline__ void epilogue32(RowState& st, const f32x16& P0, int vbase) {
-    const float g0 = max4(P0, 0), g1 = max4(P0, 1), g2 = max4(P0, 2), g3 = max4(P0, 3);
-    const float tmax = fmaxf(fmaxf(g0, g1), fmaxf(g2, g3));
-    const float mnew = fmaxf(st.m, tmax);
-    const float ml = mnew * LOG2E;
-    float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(P0[r], LOG2E, -ml));
-    st.s = s;
-    st.m = mnew;
-    if (__any(tmax > st.r1v)) {
-        if (__any(g0 > st.r1v)) records4<0>(st, P0, vbase);
-        if (__any(g1 > st.r1v)) records4<1>(st, P0, vbase);
-        if (__any(g2 > st.r1v)) records4<2>(st, P0, vbase);
-        if (__any(g3 > st.r1v)) records4<3>(st, P0, vbase);
-    }
-}
-
 template <int G>
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_logit_kernel(DecodeParams p, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -812,62 +957,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_logit_kernel(DecodePar
     for (int i = 0; i < 64; ++i) pin(hB[i]);
     RowState st;
     row_state_init(st);
-    if (s1 > s0) {
-        const rsrc_t lw_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
-        const rsrc_t lz_r = make_rsrc(p.noise + nidx + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
-        const rsrc_t lbw_r = make_rsrc(p.theta + p.off_log_b, 4u * (uint32_t)p.V1);
-        const rsrc_t lbz_r = make_rsrc(p.noise + nidx + p.off_log_b, 4u * (uint32_t)p.V1);
-        auto lsrc = [&](int s) {                                 // logit rows 64s .. 64s+63
-            StageSrc Sx;
-            Sx.w_r = lw_r; Sx.z_r = lz_r; Sx.b_r = lbw_r; Sx.bz_r = lbz_r;
-            Sx.so_a = 32768u * (uint32_t)s; Sx.so_b = Sx.so_a + 16384u;
-            Sx.bso = 256u * (uint32_t)s; Sx.bda = 0u; Sx.bdb = 128u;
-            Sx.valid = p.V1 - 64 * s;
-            return Sx;
-        };
-        Stage64Regs s64;
-        stage64_load(lsrc(s0), c.wave * 64 + lane_fresh(), s64);
-        stage64_store(lds, lsrc(s0).valid, c.sigma, c.wave * 64 + lane_fresh(), s64);
-        __syncthreads();
-        f32x16 prev0, prev1;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { prev0[r] = NEG_INF; prev1[r] = NEG_INF; }
-        for (int s = s0; s < s1; ++s) {
-            const int sn = min(s + 1, s1 - 1);
-            stage64_load(lsrc(sn), c.wave * 64 + lane_fresh(), s64);
-            const float* buf = lds + ((s - s0) & 1) * STAGE64_FLOATS;
-            const float* wsg = buf + c.sgn * (64 * LDS_ROW);
-            const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * c.sgn;
-            f32x16 acc0, acc1;
-            if constexpr (G == 4) {
-                if (c.sgn == 0) {
-                    mfma_stage64(wsg, bsg, hB, lane_fresh(), acc0, acc1);
-                    epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
-                } else {
-                    epilogue64(st, prev0, prev1, 64 * (s - 1) + 4 * (lane_fresh() >> 5));
-                    mfma_stage64(wsg, bsg, hB, lane_fresh(), acc0, acc1);
-                }
-            } else {
-                const float* w1 = wsg + 32 * c.hf * LDS_ROW;     // this wave's 32-row tile of the stage
-                const float* b1 = bsg + 32 * c.hf;
-                if (c.sgn == 0) {
-                    acc0 = mfma_tile(bias_init(b1, lane_fresh() >> 5), w1, hB, lane_fresh());
-                    epilogue32(st, prev0, 64 * (s - 1) + 32 * c.hf + 4 * (lane_fresh() >> 5));
-                } else {
-                    epilogue32(st, prev0, 64 * (s - 1) + 32 * c.hf + 4 * (lane_fresh() >> 5));
-                    acc0 = mfma_tile(bias_init(b1, lane_fresh() >> 5), w1, hB, lane_fresh());
-                }
-            }
-            stage64_store(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, c.sigma, c.wave * 64 + lane_fresh(), s64);
-            __syncthreads();
-            prev0 = acc0;
-            if constexpr (G == 4) prev1 = acc1;
-        }
-        if constexpr (G == 4)
-            epilogue64(st, prev0, prev1, 64 * (s1 - 1) + 4 * (lane_fresh() >> 5));
-        else
-            epilogue32(st, prev0, 64 * (s1 - 1) + 32 * c.hf + 4 * (lane_fresh() >> 5));
-    }
+    if (s1 > s0) logit_stages<G>(lds, p, nidx, c.wave, c.sgn, c.hf, c.sigma, hB, s0, s1, st);
     float* pb = part_ptr(p, c.wg, c.q, c.wave) + lane_fresh();
     pb[0] = st.m;
     pb[64] = st.s;

@@ -18,6 +18,16 @@ Fixtures (all .npz, loadable with allow_pickle=False):
   sgd.npz                         SGD.update (optimizers.py:38-47) driven like run_master, 3 steps
   adam_globalg64.npz              Adam.update(globalg) called directly with an fp64 globalg from the
                                   first step (the fp64 (1 - b) * g' branch while theta is still fp32)
+  decode_bench_xavier.npz         the bench workload itself (BASELINE.json configs[2] inputs: xavier theta seed
+                                  0, fc PCG64(1234) [128, 2048], the 2^27 table PCG64(123), noise seed 0,
+                                  iteration 1): FCModel._sample on the reference's 5x-duplicated 640 rows
+                                  (dataloader.py:175) for base theta and 8 table-perturbed members x 2 signs;
+                                  tokens of each image's first copy, per-step top-2 margins, logprobs, and
+                                  whether the 5 copies of every image decoded identically
+  master_ranks_grad.npz           NESMaster.compute_centered_ranks / gradient_estimate
+                                  (nic_nes_master.py:170-221) imported with placeholder redis/torchvision
+                                  modules: P = 512 tie-free fitness and a tied one, and the fp32 gradient
+                                  of 512 table-noise vectors on 4096 sampled coordinates
   fitness_criteria.npz            the greedy_* fitness criteria (src/captioning/fitness.py:43-132, chosen
                                   by Fitness.get_criterium, src/captioning/policies.py:50-61) on seeded
                                   logprobs / sequences / per-row CIDEr rewards, as CaptPolicy.rollout
@@ -116,6 +126,74 @@ def decode_fixture(name, d, theta_seed, gain, bias_std, fc_seed, B, store_theta,
         out['member_margins'] = np.stack(pmar)
     np.savez_compressed(os.path.join(OUT, name + '.npz'), **out)
     print(name, 'seq[0]', seq[0], 'min margin', float(mar.min()))
+
+
+def decode_bench_fixture():
+    d = O.Dims()
+    model = ref_model(d)
+    theta = O.make_theta(d, 0, 1.0, 0.0)               # = nicnes.synthetic.init_theta(Dims(), 0)
+    B, T_LEN, TSEED, NSEED, IT, SIGMA = 128, 1 << 27, 123, 0, 1, 0.01
+    fc = np.random.Generator(np.random.PCG64(1234)).standard_normal((B, d.F)).astype(np.float32)
+    fc5 = np.repeat(fc, 5, axis=0)                     # the reference decodes every image 5 times
+    table = O.noise_table(T_LEN, TSEED)
+    members = np.linspace(0, 511, 8).astype(np.int64)
+    seqs, mars, lps, dup = [], [], [], []
+
+    def run(th):
+        load_theta(model, th)
+        s5, lp5, m5 = ref_decode(model, fc5)
+        s5, lp5, m5 = s5.reshape(B, 5, -1), lp5.reshape(B, 5, -1), m5.reshape(B, 5, -1)
+        dup.append(bool((s5 == s5[:, :1]).all()))
+        seqs.append(s5[:, 0])
+        mars.append(m5[:, 0])
+        lps.append(lp5[:, 0])
+
+    run(theta)                                         # base theta: the synthetic references' seed captions
+    for mbr in members:
+        idx = O.noise_index(NSEED, IT, int(mbr), T_LEN, d.D)
+        for sign in (+1, -1):
+            run(O.perturb(theta, table, idx, SIGMA, sign))
+    np.savez_compressed(os.path.join(OUT, 'decode_bench_xavier.npz'), B=np.int64(B), noise_len=np.int64(T_LEN),
+                        table_seed=np.int64(TSEED), noise_seed=np.int64(NSEED), iteration=np.int64(IT),
+                        sigma=np.float64(SIGMA), members=members, seq=np.stack(seqs).astype(np.int16),
+                        margins=np.stack(mars), logprobs=np.stack(lps), dup_consistent=np.array(dup))
+    print('decode_bench: copies consistent', all(dup), 'min margin', float(np.stack(mars).min()))
+
+
+class _Placeholder(__import__('types').ModuleType):
+    """stands in for a module the reference imports but this path never uses (redis, torchvision)"""
+    def __getattr__(self, k):
+        if k.startswith('__'):
+            raise AttributeError(k)
+        return _Placeholder(self.__name__ + '.' + k)
+
+
+def master_ranks_grad_fixture():
+    np.float = float
+    for name in ('redis', 'torchvision'):
+        try:
+            __import__(name)
+        except ImportError:
+            sys.modules[name] = _Placeholder(name)
+    from algorithm.nic_nes.nic_nes_master import NESMaster   # reference module
+    master = NESMaster.__new__(NESMaster)                     # the rank/sum methods use no state
+    rng = np.random.Generator(np.random.PCG64(55))
+    P = 512
+    fit = rng.standard_normal((P, 2)) * 10.0 + 50.0          # tie-free
+    fit_ties = np.round(rng.random((P, 2)) * 40) / 4.0       # many ties
+    cr = master.compute_centered_ranks(fit)
+    cr_ties = master.compute_centered_ranks(fit_ties)
+    d = O.Dims()
+    T_LEN, NSEED, IT, SIGMA = 1 << 27, 0, 1, 0.01
+    table = O.noise_table(T_LEN, 123)
+    idx = np.array([O.noise_index(NSEED, IT, i, T_LEN, d.D) for i in range(P)], np.int64)
+    J = np.sort(np.random.Generator(np.random.PCG64(3)).choice(d.D, 4096, replace=False)).astype(np.int64)
+    vecs = np.float32(SIGMA) * table[idx[:, None] + J[None, :]]                  # delta_i[J], fp32
+    g = master.gradient_estimate(fit, vecs)
+    np.savez_compressed(os.path.join(OUT, 'master_ranks_grad.npz'), fit=fit, cr=cr, fit_ties=fit_ties,
+                        cr_ties=cr_ties, noise_len=np.int64(T_LEN), noise_seed=np.int64(NSEED),
+                        iteration=np.int64(IT), sigma=np.float64(SIGMA), idx=idx, J=J, grad=np.asarray(g))
+    print('master: grad dtype', np.asarray(g).dtype, 'max|g|', float(np.abs(g).max()))
 
 
 def perturb_fixture():
@@ -240,6 +318,8 @@ def all_fixtures():
     sgd_fixture()
     adam_globalg64_fixture()
     fitness_criteria_fixture()
+    decode_bench_fixture()
+    master_ranks_grad_fixture()
 
 
 if __name__ == '__main__':

@@ -145,3 +145,58 @@ def test_shared_math_accuracy():
         ulp = np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
         ok = np.abs(ref) > 1e-30
         assert (np.abs(y - ref)[ok] / ulp[ok]).max() < 3.0, name
+
+
+def _bench_inputs(z):
+    d = O.Dims()
+    theta = O.make_theta(d, 0, 1.0, 0.0)
+    fc = np.random.Generator(np.random.PCG64(1234)).standard_normal((int(z['B']), d.F)).astype(np.float32)
+    table = O.noise_table(int(z['noise_len']), int(z['table_seed']))
+    thetas = [theta]
+    for mbr in z['members']:
+        idx = O.noise_index(int(z['noise_seed']), int(z['iteration']), int(mbr), int(z['noise_len']), d.D)
+        thetas += [O.perturb(theta, table, idx, float(z['sigma']), sign) for sign in (+1, -1)]
+    return d, fc, thetas
+
+
+def test_bench_workload_decode_matches_reference(golden_dir):
+    """The benchmarked workload itself (xavier theta, B = 128, the 2^27 table, 8 members x 2 signs + base
+    theta) against FCModel._sample run by scripts/make_golden.py on the reference's 640 duplicated rows:
+    every row identical end to end, near-tie steps included (217 steps with a top-2 margin < 1e-5, 12
+    exact ties at generation time), and the 5 copies of each image decoded identically by the reference."""
+    z = np.load(golden_dir + '/decode_bench_xavier.npz')
+    assert z['dup_consistent'].all()
+    d, fc, thetas = _bench_inputs(z)
+    ref = z['seq'].astype(np.int32)
+    assert (z['margins'] < MARGIN).sum() > 100           # the fixture exercises near ties
+    for k, th in enumerate(thetas):
+        seq, lp, fr = O.decode(d, th, fc)
+        assert np.array_equal(seq, ref[k]), (k, np.argwhere(seq != ref[k])[:3])
+        live = z['logprobs'][k] != 0
+        assert np.allclose(lp[live], z['logprobs'][k][live], atol=5e-6)
+
+
+def test_master_ranks_and_gradient_match_reference(golden_dir):
+    """NESMaster.compute_centered_ranks / gradient_estimate (nic_nes_master.py:170-221), imported by
+    scripts/make_golden.py: P = 512. Tie-free fitness: ranks bit-exact. Tied fitness: the reference's
+    default (unstable) argsort orders equal values arbitrarily, the restatement by position; each group
+    of equal values gets the same set of ranks. Gradient: fp64-accumulated restatement vs the reference's
+    fp32 np.dot groups, within 1e-6 of max |g| (north_star allows 1e-5)."""
+    z = np.load(golden_dir + '/master_ranks_grad.npz')
+    cr = O.compute_centered_ranks(z['fit'])
+    assert np.array_equal(cr, z['cr'])
+    cr_t = O.compute_centered_ranks(z['fit_ties'])
+    x, a, b = z['fit_ties'].ravel(), cr_t.ravel(), z['cr_ties'].ravel()
+    for v in np.unique(x):
+        assert np.array_equal(np.sort(a[x == v]), np.sort(b[x == v])), v
+    table = O.noise_table(int(z['noise_len']), 123)
+    J, idx = z['J'], z['idx']
+    w, _ = O.weights_from_fitness(z['fit'])
+    acc = np.zeros(J.size, np.float64)
+    s = np.float32(z['sigma'])
+    for i in range(idx.size):
+        acc += np.float64(w[i]) * (s * table[idx[i] + J]).astype(np.float64)
+    g = acc.astype(np.float32) / np.float32(2 * idx.size)
+    assert np.abs(g - z['grad']).max() <= 1e-6 * np.abs(z['grad']).max()
+    assert [O.noise_index(int(z['noise_seed']), int(z['iteration']), i, int(z['noise_len']), O.Dims().D)
+            for i in (0, 511)] == [int(idx[0]), int(idx[511])]
