@@ -40,18 +40,18 @@ NN_FN float nn_floorf(float x) {
 NN_FN float nn_pow2i(int32_t n) { return nn_i2f((n + 127) << 23); }
 
 /*
- * nn_expf: e^x, <= ~1 ulp. Cody-Waite reduction x = n ln2 + r, |r| <= ln2/2,
- * degree-7 Taylor in Horner form with fmaf, then scale by 2^n in two steps so
- * results in the subnormal range are formed exactly like on the host.
- * Branch-free: the core runs on x clamped to [-104, 89] and the out-of-range / NaN results are
- * selected at the end (one instruction stream for every lane of a wavefront); the values are
- * those of the branchy form (tests/test_oracle_golden.py checks both against each other).
+ * nn_expf: e^x, <= ~1 ulp on the range the hot path uses. Cody-Waite reduction x = n ln2 + r,
+ * |r| <= ln2/2, degree-7 Taylor in Horner form with fmaf, one scale by 2^n. The argument is
+ * clamped to [-87, 88] so the scale stays a normal power of two (below -87 the result is e^-87
+ * instead of a subnormal or 0: every caller adds it to 1 or multiplies a bounded value by it);
+ * above 88.72 the result is +inf and NaN passes through. Branch-free (one instruction stream for
+ * every lane of a wavefront).
  */
 NN_FN float nn_expf(float x) {
     const float log2e = 1.44269502162933349609375f;
     const float ln2_hi = 0.693145751953125f;          /* 12 significant bits: n*ln2_hi exact */
     const float ln2_lo = 1.428606765330187045e-06f;
-    const float xc = fminf(fmaxf(x, -104.0f), 89.0f); /* NaN -> -104 (replaced below) */
+    const float xc = fminf(fmaxf(x, -87.0f), 88.0f);  /* NaN -> -87 (replaced below) */
     float n = nn_floorf(xc * log2e + 0.5f);
     float r = fmaf(-n, ln2_hi, xc);
     r = fmaf(-n, ln2_lo, r);
@@ -63,16 +63,34 @@ NN_FN float nn_expf(float x) {
     p = fmaf(p, r, 0.5f);
     p = fmaf(p, r, 1.0f);
     p = fmaf(p, r, 1.0f);
-    const int32_t ni = (int32_t)n;                    /* in [-150, 129] */
-    const int32_t n1 = ni > 127 ? 127 : (ni < -126 ? -126 : ni);
-    float y = p * nn_pow2i(n1) * nn_pow2i(ni - n1);   /* second factor 2^0 unless out of range */
+    float y = p * nn_pow2i((int32_t)n);               /* n in [-126, 127] */
     y = x > 88.72283935546875f ? nn_i2f(0x7f800000) : y;
-    y = x < -103.972084045410156f ? 0.0f : y;
     return x != x ? x : y;
 }
 
-/* sigmoid as torch.sigmoid defines it (src/captioning/nets.py:117): 1 / (1 + e^-x) */
-NN_FN float nn_sigmoidf(float x) { return 1.0f / (1.0f + nn_expf(-x)); }
+/*
+ * nn_rcp1f: 1/d for d in [1, 2^120], <= ~1 ulp: integer first guess (relative error < 12.5 %) and
+ * three Newton steps e = 1 - d y, y += y e in fmaf (error squares each step: 1.6e-2, 2.4e-4,
+ * 5.9e-8 before the last rounding). Deterministic IEEE operations only, so host and GPU agree.
+ */
+NN_FN float nn_rcp1f(float d) {
+    float y = nn_i2f(0x7EF311C3 - nn_f2i(d));
+    float e = fmaf(-d, y, 1.0f);
+    y = fmaf(y, e, y);
+    e = fmaf(-d, y, 1.0f);
+    y = fmaf(y, e, y);
+    e = fmaf(-d, y, 1.0f);
+    return fmaf(y, e, y);
+}
+
+/* sigmoid as torch.sigmoid defines it (src/captioning/nets.py:117): 1 / (1 + e^-x); the argument is
+ * clamped to [-80, 80] (sigmoid there is 1 - 2^-115 .. 2^-115 off its limit) so 1 + e^-x stays in the
+ * reciprocal's range */
+NN_FN float nn_sigmoidf(float x) {
+    const float xc = fminf(fmaxf(x, -80.0f), 80.0f);
+    const float y = nn_rcp1f(1.0f + nn_expf(-xc));
+    return x != x ? x : y;
+}
 
 /*
  * nn_tanhf: odd; |x| < 0.6 -> x * P(x^2) (least-squares fit of tanh(x)/x in double,
@@ -90,10 +108,12 @@ NN_FN float nn_tanhf(float x) {
     p = fmaf(p, u, -0.3333333134651184f);
     p = fmaf(p, u, 1.0f);
     const float small = x * p;
-    float y = 1.0f - 2.0f / (nn_expf(2.0f * a) + 1.0f);
+    const float ac = a > 9.5f ? 9.5f : a;             /* e^19 + 1 < 2^28: in the reciprocal's range */
+    float y = 1.0f - 2.0f * nn_rcp1f(nn_expf(2.0f * ac) + 1.0f);
     y = a > 9.5f ? 1.0f : y;
     y = x < 0.0f ? -y : y;
-    return a < 0.6f ? small : y;
+    y = a < 0.6f ? small : y;
+    return x != x ? x : y;
 }
 
 /*
