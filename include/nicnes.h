@@ -140,6 +140,25 @@ int nicnes_sgd_step(nicnes_handle* h, const float* gsum, int32_t P, double l2coe
 int nicnes_optimizer_update(nicnes_handle* h, int kind, const double* globalg, int globalg_fp32, double stepsize,
                             double beta1, double beta2, double epsilon, double* ratio_out_host, void* stream);
 
+/* Multi-GPU data plane: one handle per GPU, one rank per handle. The reference
+ * has no collective -- its master gathers every worker's 11.46 MB noise vector over redis and sums
+ * them in gradient_estimate (src/dist.py:90-93,199-201, src/algorithm/nic_nes/nic_nes_master.py:
+ * 92-123,170-182); the engine exchanges the (P, 2) fitness and one D-float noise sum over RCCL.
+ * nicnes_comm_unique_id: rank 0 makes the 128-byte id and sends it to the other ranks out of band;
+ * nicnes_comm_init: every rank joins (collective, blocking); nicnes_comm_attach borrows an
+ * ncclComm_t the caller already owns (e.g. torch.distributed's); nicnes_comm_destroy releases. */
+#define NICNES_COMM_ID_BYTES 128
+int nicnes_comm_unique_id(uint8_t* id_out_host);
+int nicnes_comm_init(nicnes_handle* h, int32_t nranks, int32_t rank, const uint8_t* id_host);
+int nicnes_comm_attach(nicnes_handle* h, void* nccl_comm);
+int nicnes_comm_destroy(nicnes_handle* h);
+/* fit_all [P_local * nranks, 2] fp64 <- every rank's fit_local [P_local, 2], in rank order, so every
+ * rank then ranks the whole population identically (compute_centered_ranks needs all 2P values). */
+int nicnes_allgather_fitness(nicnes_handle* h, const double* fit_local, int32_t P_local, double* fit_all, void* stream);
+/* gsum [D] fp32 summed in place over the ranks: the shards' nicnes_grad_partial results become the
+ * whole population's noise sum before nicnes_adam_step (batched_weighted_sum, nic_nes_master.py:207-221). */
+int nicnes_allreduce_grad(nicnes_handle* h, float* gsum, void* stream);
+
 /* diagnostics: [0] = exact-pass fallbacks of the greedy tie rule since creation (synchronising) */
 int nicnes_stats(nicnes_handle* h, int64_t* out4_host);
 

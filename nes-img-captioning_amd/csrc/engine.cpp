@@ -13,6 +13,8 @@
 #include <vector>
 #include <algorithm>
 
+#include <rccl/rccl.h>
+
 #include "../../include/nicnes.h"
 #include "cider_kernel.h"
 #include "decode_kernel.h"
@@ -77,6 +79,10 @@ struct nicnes_handle {
     int dec_S = 0, dec_G = 0;         // nicnes_set_decode_split (0 = automatic)
     double* partials = nullptr;
     double* norms = nullptr;
+
+    ncclComm_t comm = nullptr;        // population shards over ranks (nicnes_comm_init / _attach)
+    bool comm_owned = false;
+    int comm_nranks = 1;
 
     bool timing = false;
     int force_exact = 0;      // test hook: exact tie pass on every step (NICNES_FORCE_EXACT=1)
@@ -167,6 +173,49 @@ void decode_shape(const nicnes_handle* h, int B, int count, int* G, int* nslabs,
     *S = h->dec_S ? h->dec_S : auto_split((int64_t)count * *nslabs, h->n_cu, *G);
 }
 
+// Buffers sized by the reference count: the cooked reference n-gram vectors (CIDEr-D).
+int alloc_refs(nicnes_handle* h, int max_refs) {
+    void* old[] = {h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2, h->ref_norm};
+    for (void* q : old)
+        if (q) (void)hipFree(q);
+    h->ref_keys = nullptr; h->ref_vec = nullptr; h->ref_count = nullptr; h->ref_len2 = nullptr; h->ref_norm = nullptr;
+    const size_t MR = (size_t)max_refs;
+    int rc = dalloc(h, &h->ref_keys, MR * 64);
+    if (!rc) rc = dalloc(h, &h->ref_vec, MR * 64);
+    if (!rc) rc = dalloc(h, &h->ref_count, MR);
+    if (!rc) rc = dalloc(h, &h->ref_len2, MR);
+    if (!rc) rc = dalloc(h, &h->ref_norm, MR * 4);
+    if (!rc) h->cfg.max_refs = max_refs;
+    return rc;
+}
+
+// Buffers sized by the batch: per-image n-gram tables, tokens / log-probs / row scores of a launch,
+// decode lane scratch, alive flags and partial states.
+int alloc_batch(nicnes_handle* h, int max_batch) {
+    void* old[] = {h->img_hkey, h->img_hrow, h->img_vr, h->seq, h->lp, h->row_scores, h->dscratch, h->alive, h->part};
+    for (void* q : old)
+        if (q) (void)hipFree(q);
+    h->img_hkey = nullptr; h->img_hrow = nullptr; h->img_vr = nullptr; h->seq = nullptr; h->lp = nullptr;
+    h->row_scores = nullptr; h->dscratch = nullptr; h->alive = nullptr; h->part = nullptr;
+    const size_t MM = (size_t)h->cfg.max_members, MB = (size_t)max_batch, T = (size_t)h->cfg.seq_length;
+    // lane scratch: 2G row waves per slab, the larger of the two slab layouts
+    const int rw = std::max(8 * nslabs_of((int)MB, 4), 4 * nslabs_of((int)MB, 2));
+    h->alive_stride = (int32_t)(MM * (size_t)nslabs_of((int)MB, 2));
+    const int ns = std::max(nslabs_of((int)MB, 2), nslabs_of((int)MB, 4));
+    h->part_cap = std::max(auto_part_cap((int)MM, (int)MB, h->n_cu), (int64_t)MM * ns * std::max(h->dec_S, 1));
+    int rc = dalloc(h, &h->img_hkey, MB * IMG_CAP);
+    if (!rc) rc = dalloc(h, &h->img_hrow, MB * IMG_CAP);
+    if (!rc) rc = dalloc(h, &h->img_vr, MB * IMG_ROWS * IMG_MAXR);
+    if (!rc) rc = dalloc(h, &h->seq, MM * 2 * MB * T);
+    if (!rc) rc = dalloc(h, &h->lp, MM * 2 * MB * T);
+    if (!rc) rc = dalloc(h, &h->row_scores, MM * 2 * MB);
+    if (!rc) rc = dalloc(h, &h->dscratch, nicnes_decode_scratch_floats((int)MM, rw));
+    if (!rc) rc = dalloc(h, &h->alive, 3 * (size_t)h->alive_stride);
+    if (!rc) rc = dalloc(h, &h->part, (size_t)h->part_cap * PART_FLOATS);
+    if (!rc) h->cfg.max_batch = max_batch;
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -212,25 +261,13 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
         delete h;
         return NICNES_ERR_HIP;
     }
-    const size_t D = (size_t)h->D, MR = (size_t)cfg->max_refs, MM = (size_t)cfg->max_members,
-                 MB = (size_t)cfg->max_batch, T = (size_t)cfg->seq_length;
+    const size_t D = (size_t)h->D, MM = (size_t)cfg->max_members;
     int rc = NICNES_OK;
     if (!rc) rc = dalloc(h, &h->theta64, D);
     if (!rc) rc = dalloc(h, &h->theta32, D);
     if (!rc) rc = dalloc(h, &h->m, D);
     if (!rc) rc = dalloc(h, &h->v, D);
-    if (!rc) rc = dalloc(h, &h->ref_keys, MR * 64);
-    if (!rc) rc = dalloc(h, &h->ref_vec, MR * 64);
-    if (!rc) rc = dalloc(h, &h->ref_count, MR);
-    if (!rc) rc = dalloc(h, &h->ref_len2, MR);
-    if (!rc) rc = dalloc(h, &h->ref_norm, MR * 4);
-    if (!rc) rc = dalloc(h, &h->img_hkey, MB * IMG_CAP);
-    if (!rc) rc = dalloc(h, &h->img_hrow, MB * IMG_CAP);
-    if (!rc) rc = dalloc(h, &h->img_vr, MB * IMG_ROWS * IMG_MAXR);
     if (!rc) rc = dalloc(h, &h->nidx, MM);
-    if (!rc) rc = dalloc(h, &h->seq, MM * 2 * MB * T);
-    if (!rc) rc = dalloc(h, &h->lp, MM * 2 * MB * T);
-    if (!rc) rc = dalloc(h, &h->row_scores, MM * 2 * MB);
     {
         const char* fe = getenv("NICNES_FORCE_EXACT");
         h->force_exact = (fe && fe[0] == '1') ? 1 : 0;
@@ -241,16 +278,11 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
             h->n_cu = ncu;
     }
     if (!rc && nicnes_decode_init() != hipSuccess) rc = fail(h, NICNES_ERR_HIP, "nicnes_decode_init");
-    // lane scratch: 2G row waves per slab, the larger of the two slab layouts
-    const int rw = std::max(8 * nslabs_of((int)MB, 4), 4 * nslabs_of((int)MB, 2));
-    h->alive_stride = (int32_t)(MM * (size_t)nslabs_of((int)MB, 2));
-    h->part_cap = auto_part_cap((int)MM, (int)MB, h->n_cu);
-    if (!rc) rc = dalloc(h, &h->dscratch, nicnes_decode_scratch_floats((int)MM, rw));
     if (!rc) rc = dalloc(h, &h->stats, 4);
-    if (!rc) rc = dalloc(h, &h->alive, 3 * (size_t)h->alive_stride);
-    if (!rc) rc = dalloc(h, &h->part, (size_t)h->part_cap * PART_FLOATS);
     if (!rc) rc = dalloc(h, &h->partials, 2 * (size_t)nicnes_adam_blocks(h->D));
     if (!rc) rc = dalloc(h, &h->norms, 2);
+    if (!rc) rc = alloc_refs(h, cfg->max_refs);
+    if (!rc) rc = alloc_batch(h, cfg->max_batch);
     if (rc) {
         nicnes_destroy(h);
         return rc;
@@ -269,6 +301,7 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
 int nicnes_destroy(nicnes_handle* h) {
     if (!h) return NICNES_OK;
     (void)hipSetDevice(h->device);
+    if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
                     h->ref_norm, h->nidx, h->seq, h->lp, h->row_scores, h->dscratch, h->stats, h->partials, h->norms,
                     h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive, h->part};
@@ -385,11 +418,24 @@ int nicnes_set_df_table(nicnes_handle* h, const uint64_t* keys, const double* df
 int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t* ref_tokens, int32_t n_refs,
                      const int32_t* img_ref_start, void* stream) {
     if (!h || !fc || !ref_tokens || !img_ref_start) return NICNES_ERR_INVALID;
-    if (B < 1 || B > h->cfg.max_batch) return fail(h, NICNES_ERR_INVALID, "B out of [1, max_batch]");
-    if (n_refs < B || n_refs > h->cfg.max_refs) return fail(h, NICNES_ERR_INVALID, "n_refs out of [B, max_refs]");
+    if (B < 1 || B > 1024) return fail(h, NICNES_ERR_INVALID, "B out of [1, 1024]");
+    if (n_refs < B) return fail(h, NICNES_ERR_INVALID, "n_refs < B");
     if (!h->df_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_df_table first");
     if (((uintptr_t)fc & 15u) != 0) return fail(h, NICNES_ERR_INVALID, "fc must be 16-byte aligned");
     HIPC(h, hipSetDevice(h->device));
+    // a batch-size curriculum (bs_multiplier, tools/iteration.py:149-153) can outgrow the sizes the
+    // handle was created with: re-create the batch buffers (outside every evaluate, so no launch
+    // in flight uses them once the device is idle)
+    if (B > h->cfg.max_batch || n_refs > h->cfg.max_refs) {
+        HIPC(h, hipDeviceSynchronize());
+        int rc = NICNES_OK;
+        if (n_refs > h->cfg.max_refs) rc = alloc_refs(h, std::max(n_refs, 2 * h->cfg.max_refs));
+        if (!rc && B > h->cfg.max_batch) rc = alloc_batch(h, B);
+        if (rc) {
+            h->batch_set = false;
+            return rc;
+        }
+    }
     // reference ranges: CiderD asserts every image has references (len(ref) > 0, upstream
     // cider_scorer); ranges must tile [0, n_refs)
     std::vector<int32_t> st((size_t)B + 1);
@@ -681,6 +727,73 @@ int nicnes_set_decode_split(nicnes_handle* h, int32_t S, int32_t G) {
     }
     h->dec_S = S;
     h->dec_G = G;
+    return NICNES_OK;
+}
+
+// ---- multi-GPU exchange over RCCL (the data plane of SURVEY.md 8(e)) ---------------------------
+#define NCCLC(h, expr)                                                                          \
+    do {                                                                                        \
+        ncclResult_t r_ = (expr);                                                               \
+        if (r_ != ncclSuccess)                                                                  \
+            return fail((h), NICNES_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+int nicnes_comm_unique_id(uint8_t* id_out_host) {
+    if (!id_out_host) return NICNES_ERR_INVALID;
+    static_assert(sizeof(ncclUniqueId) == NICNES_COMM_ID_BYTES, "RCCL unique id size");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return NICNES_ERR_HIP;
+    std::memcpy(id_out_host, &id, sizeof id);
+    return NICNES_OK;
+}
+
+int nicnes_comm_init(nicnes_handle* h, int32_t nranks, int32_t rank, const uint8_t* id_host) {
+    if (!h || !id_host || nranks < 1 || rank < 0 || rank >= nranks) return NICNES_ERR_INVALID;
+    if (h->comm) return fail(h, NICNES_ERR_INVALID, "a communicator is already bound (nicnes_comm_destroy first)");
+    HIPC(h, hipSetDevice(h->device));
+    ncclUniqueId id;
+    std::memcpy(&id, id_host, sizeof id);
+    ncclComm_t c = nullptr;
+    NCCLC(h, ncclCommInitRank(&c, nranks, id, rank));
+    h->comm = c;
+    h->comm_owned = true;
+    h->comm_nranks = nranks;
+    return NICNES_OK;
+}
+
+int nicnes_comm_attach(nicnes_handle* h, void* nccl_comm) {
+    if (!h || !nccl_comm) return NICNES_ERR_INVALID;
+    if (h->comm) return fail(h, NICNES_ERR_INVALID, "a communicator is already bound (nicnes_comm_destroy first)");
+    int n = 0;
+    NCCLC(h, ncclCommCount((ncclComm_t)nccl_comm, &n));
+    h->comm = (ncclComm_t)nccl_comm;
+    h->comm_owned = false;
+    h->comm_nranks = n;
+    return NICNES_OK;
+}
+
+int nicnes_comm_destroy(nicnes_handle* h) {
+    if (!h) return NICNES_ERR_INVALID;
+    if (h->comm && h->comm_owned) NCCLC(h, ncclCommDestroy(h->comm));
+    h->comm = nullptr;
+    h->comm_owned = false;
+    h->comm_nranks = 1;
+    return NICNES_OK;
+}
+
+int nicnes_allgather_fitness(nicnes_handle* h, const double* fit_local, int32_t P_local, double* fit_all, void* stream) {
+    if (!h || !fit_local || !fit_all || P_local < 1) return NICNES_ERR_INVALID;
+    if (!h->comm) return fail(h, NICNES_ERR_INVALID, "no communicator (nicnes_comm_init / nicnes_comm_attach)");
+    HIPC(h, hipSetDevice(h->device));
+    NCCLC(h, ncclAllGather(fit_local, fit_all, (size_t)P_local * 2, ncclDouble, h->comm, (hipStream_t)stream));
+    return NICNES_OK;
+}
+
+int nicnes_allreduce_grad(nicnes_handle* h, float* gsum, void* stream) {
+    if (!h || !gsum) return NICNES_ERR_INVALID;
+    if (!h->comm) return fail(h, NICNES_ERR_INVALID, "no communicator (nicnes_comm_init / nicnes_comm_attach)");
+    HIPC(h, hipSetDevice(h->device));
+    NCCLC(h, ncclAllReduce(gsum, gsum, (size_t)h->D, ncclFloat, ncclSum, h->comm, (hipStream_t)stream));
     return NICNES_OK;
 }
 

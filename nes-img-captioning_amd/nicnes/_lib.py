@@ -6,6 +6,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libnicnes.so')
 
 OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_HIP, ERR_NOMEM = 0, 1, 2, 3, 4
+COMM_ID_BYTES = 128
 _NAMES = {ERR_INVALID: 'invalid argument', ERR_UNSUPPORTED: 'not supported', ERR_HIP: 'HIP error',
           ERR_NOMEM: 'out of device memory'}
 
@@ -16,7 +17,8 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_evaluate', 'nicnes_rank_weights', 'nicnes_grad_partial', 'nicnes_adam_step', 'nicnes_stats',
            'nicnes_set_timing', 'nicnes_kernel_times', 'nicnes_decode_phase_times', 'nicnes_sgd_step',
            'nicnes_optimizer_update', 'nicnes_last_ratio', 'nicnes_set_fitness_mode', 'nicnes_evaluate_lp',
-           'nicnes_set_decode_split', 'nicnes_decode_shape']
+           'nicnes_set_decode_split', 'nicnes_decode_shape', 'nicnes_comm_unique_id', 'nicnes_comm_init',
+           'nicnes_comm_attach', 'nicnes_comm_destroy', 'nicnes_allgather_fitness', 'nicnes_allreduce_grad']
 
 
 class NicnesConfig(ctypes.Structure):
@@ -71,6 +73,12 @@ def lib(path=None):
         'nicnes_decode_phase_times': (c.c_int, [vp, vp]),
         'nicnes_set_decode_split': (c.c_int, [vp, i32, i32]),
         'nicnes_decode_shape': (c.c_int, [vp, i32, i32, vp]),
+        'nicnes_comm_unique_id': (c.c_int, [vp]),
+        'nicnes_comm_init': (c.c_int, [vp, i32, i32, vp]),
+        'nicnes_comm_attach': (c.c_int, [vp, vp]),
+        'nicnes_comm_destroy': (c.c_int, [vp]),
+        'nicnes_allgather_fitness': (c.c_int, [vp, vp, i32, vp, vp]),
+        'nicnes_allreduce_grad': (c.c_int, [vp, vp, vp]),
         'nicnes_last_ratio': (c.c_int, [vp, vp, vp]),
         'nicnes_sgd_step': (c.c_int, [vp, vp, i32, f64, f64, f64, vp, vp]),
         'nicnes_optimizer_update': (c.c_int, [vp, c.c_int, vp, c.c_int, f64, f64, f64, f64, vp, vp]),

@@ -267,6 +267,38 @@ class Engine:
         check(self.L.nicnes_decode_shape(self.h, int(B or self.B), int(count), out), self.h, 'decode_shape')
         return tuple(int(v) for v in out)
 
+    # ---------------------------------------------------------------- multi-GPU (RCCL) ----------
+    @staticmethod
+    def comm_unique_id():
+        """128-byte RCCL id, made by rank 0 and sent to the other ranks out of band."""
+        buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES)()
+        check(_lib.lib().nicnes_comm_unique_id(buf), None, 'comm_unique_id')
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        """Join the RCCL communicator `uid` as `rank` of `nranks` (collective over the ranks)."""
+        buf = (ctypes.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(uid)
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_comm_init(self.h, int(nranks), int(rank), buf), self.h, 'comm_init')
+        self.comm_ranks = int(nranks)
+
+    def comm_destroy(self):
+        check(self.L.nicnes_comm_destroy(self.h), self.h, 'comm_destroy')
+        self.comm_ranks = 1
+
+    def allgather_fitness(self, fit_local, fit_all):
+        """fit_all [P_local * nranks, 2] <- every rank's fit_local [P_local, 2] (rank order)."""
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_allgather_fitness(self.h, _ptr(fit_local), int(fit_local.shape[0]), _ptr(fit_all),
+                                                  self._stream()), self.h, 'allgather_fitness')
+        return fit_all
+
+    def allreduce_grad(self, gsum):
+        """gsum [D] fp32 summed in place over the ranks."""
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_allreduce_grad(self.h, _ptr(gsum), self._stream()), self.h, 'allreduce_grad')
+        return gsum
+
     def stats(self):
         out = (ctypes.c_int64 * 4)()
         check(self.L.nicnes_stats(self.h, out), self.h, 'stats')

@@ -77,10 +77,10 @@ class Schedule:
 
 
 class EngineMaster:
-    def __init__(self, spec, engine, log_dir=None, rank=0, world_size=1, group=None, theta=None):
+    def __init__(self, spec, engine, log_dir=None, rank=0, world_size=1, group=None, theta=None, comm=None):
         self.spec, self.e = spec, engine
         self.log_dir = log_dir or spec.config.log_dir or 'logs/nicnes'
-        self.rank, self.world, self.group = rank, world_size, group
+        self.rank, self.world, self.group, self.comm = rank, world_size, group, comm
         self.sched = Schedule(spec.config, spec.nb_offspring)
         self.policy = EnginePolicy(engine, spec)
         if theta is not None:
@@ -91,10 +91,11 @@ class EngineMaster:
 
     # ------------------------------------------------------------------------ helpers ----------
     def _set_batch(self, batch):
-        fc, gts = unique_batch(batch) if isinstance(batch, dict) else batch
-        if id(batch) != self._batch_key:
+        # the batch object itself is kept: an id() of a freed batch can be reused by the next one
+        if batch is not self._batch_key:
+            fc, gts = unique_batch(batch) if isinstance(batch, dict) else batch
             self.e.set_batch(fc, gts)
-            self._batch_key = id(batch)
+            self._batch_key = batch
 
     def _update(self, gsum, P):
         return self.opt.update_from_noise_sum(gsum, P, self.spec.l2coeff)
@@ -112,38 +113,59 @@ class EngineMaster:
         if self.rank == 0 and freq and self.sched.iteration % freq == 0:
             self.save_snapshot()
 
+    def _after_update(self):
+        """nic_nes_master.py:139-141,161-163: when the schedule is reached the Adam step size is
+        divided by stepsize_divisor (the noise / batch curriculum already moved in incr_iteration)."""
+        if self.sched.schedule_reached and self.spec.config.stepsize_divisor:
+            self.opt.stepsize /= self.spec.config.stepsize_divisor
+
+    def _batch_stream(self, batches):
+        """Yield one batch per iteration. A loader (an object with get_batch, e.g. data.CocoFcDataLoader)
+        is asked for batches of the CURRENT scheduled size, so a bs_multiplier curriculum changes what
+        is evaluated (the reference restarts its loader with the new size, tools/iteration.py:150-154);
+        any other iterable is consumed as given, one pass per epoch."""
+        if hasattr(batches, 'get_batch'):
+            while True:
+                yield batches.get_batch('train', batch_size=self.sched.batch_size)
+        for b in batches:
+            yield b
+
     # ------------------------------------------------------------------------ loops ------------
     def run(self, batches, max_iterations=None):
         """Single-node loop: every rank evaluates its shard of the population; one all-gather of the
-        fitness and one all-reduce of the noise sum per iteration (population.py)."""
+        fitness and one all-reduce of the noise sum per iteration (population.py). `batches`: a loader
+        (batches drawn at the scheduled batch size) or an iterable of batches, re-iterated per epoch;
+        an iterable that yields nothing ends the run."""
         P = self.spec.nb_offspring
         max_it = max_iterations or self.spec.config.max_nb_iterations
         runner = None
         while not max_it or self.sched.iteration < max_it:
             self.sched.epoch += 1
-            for batch in batches:
+            yielded = False
+            for batch in self._batch_stream(batches):
+                yielded = True
                 t0 = time.time()
                 self.sched.incr_iteration()
                 self._set_batch(batch)
                 if runner is None or runner.sigma != self.sched.noise_stdev:
                     runner = PopulationRunner(self.e, P, self.sched.noise_stdev, rank=self.rank,
-                                              world_size=self.world, group=self.group)
+                                              world_size=self.world, group=self.group, comm=self.comm)
                 runner.evaluate(self.sched.iteration)
                 fit = runner.exchange_fitness()
                 _, w = self.e.rank_weights(fit)
                 self.e.grad_partial(self.sched.iteration, runner.m0, runner.local,
                                     w[runner.m0:runner.m0 + runner.local], self.sched.noise_stdev, out=runner.gsum)
-                if self.world > 1:
-                    torch.distributed.all_reduce(runner.gsum, group=self.group)
+                runner.reduce_noise_sum()
                 ratio = self._update(runner.gsum, P)
                 self._record(fit, ratio, t0)
-                if self.sched.schedule_reached and self.spec.config.stepsize_divisor:
-                    self.opt.stepsize /= self.spec.config.stepsize_divisor
+                self._after_update()
                 self._maybe_snapshot()
                 if max_it and self.sched.iteration >= max_it:
                     return self.stats
-                if self.sched.schedule_reached:
-                    break          # batch size changed: the caller's loader yields new batches
+                if self.sched.schedule_reached and not hasattr(batches, 'get_batch'):
+                    break          # batch size changed: the caller's iterable yields new batches
+            if not yielded:
+                return self.stats  # an exhausted one-shot iterator: nothing more to evaluate
         return self.stats
 
     def current_model_path(self):
@@ -166,7 +188,7 @@ class EngineMaster:
         P = self.spec.nb_offspring
         client.declare_experiment(self.spec.exp)
         done = 0
-        for batch in batches:
+        for batch in self._batch_stream(batches):
             if done >= max_iterations:
                 break
             t0 = time.time()
@@ -193,6 +215,7 @@ class EngineMaster:
             gsum = self.e.grad_partial(self.sched.iteration, 0, P, w, sigma)
             ratio = self._update(gsum, P)
             self._record(fit, ratio, t0)
+            self._after_update()
             self._maybe_snapshot()
             done += 1
         return self.stats

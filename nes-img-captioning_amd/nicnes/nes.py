@@ -124,12 +124,13 @@ class EnginePolicy:
         return int(self.e.noise_indices(iteration, member, 1).cpu()[0])
 
     def _ensure_batch(self, data, seq_per_img=5):
-        fc, gts = unique_batch(data, seq_per_img)
-        key = (id(data), fc.shape)
-        if key != self._batch_key:
+        # the batch object itself is kept: an id() of a freed batch can be reused by the next one
+        if data is not self._batch_key:
+            fc, gts = unique_batch(data, seq_per_img)
             self.e.set_batch(fc, gts)
-            self._batch_key = key
-        return fc.shape[0]
+            self._batch_key = data
+            self._batch_rows = fc.shape[0]
+        return self._batch_rows
 
     def rollout(self, placeholder, data, config):
         """CaptPolicy.rollout (policies.py:86-128) of the current theta: float(100 * mean CIDEr-D) for
@@ -152,10 +153,12 @@ class EngineWorker:
     def _prepare(self, task_id, task_data):
         # theta and batch are loaded once per task (the reference reloads them per member)
         cur = task_data.current
-        key = (task_id, cur if isinstance(cur, str) else id(cur))
-        if cur is not None and key != getattr(self, '_cur', None):
+        prev = getattr(self, '_cur', None)
+        # a path is compared by value within a task; any other model object by identity (kept alive)
+        same = prev is not None and prev[0] == task_id and (prev[1] == cur if isinstance(cur, str) else prev[1] is cur)
+        if cur is not None and not same:
             self.policy.set_model(cur)
-            self._cur = key
+            self._cur = (task_id, cur)
         if task_data.batch_data is not None:
             self.policy._ensure_batch(task_data.batch_data)
 
@@ -250,10 +253,11 @@ class Adam(_EngineOptimizer):
         return self.e.adam_step(gsum, P, l2coeff, self.stepsize, self.beta1, self.beta2, self.epsilon)
 
     def save_to_file(self, path):
-        """optimizer.tar with the reference keys (optimizers.py:85-95); m, v as fp64 tensors."""
+        """optimizer.tar with the reference keys and types (optimizers.py:85-95): m, v as fp64 numpy
+        arrays, so the reference's load_from_file gets the numpy state it expects."""
         m, v, t = self.e.adam_state()
         torch.save({'dim': self.dim, 't': t, 'stepsize': self.stepsize, 'beta1': self.beta1, 'beta2': self.beta2,
-                    'epsilon': self.epsilon, 'm': m.cpu(), 'v': v.cpu()}, path)
+                    'epsilon': self.epsilon, 'm': m.cpu().numpy(), 'v': v.cpu().numpy()}, path)
 
     def load_from_file(self, path):
         state = _load_state(path)
@@ -277,8 +281,8 @@ class SGD(_EngineOptimizer):
 
     def save_to_file(self, path):
         _, v, t = self.e.adam_state()
-        torch.save({'dim': self.dim, 't': t, 'momentum': self.momentum, 'stepsize': self.stepsize, 'v': v.cpu()},
-                   path)
+        torch.save({'dim': self.dim, 't': t, 'momentum': self.momentum, 'stepsize': self.stepsize,
+                    'v': v.cpu().numpy()}, path)
 
     def load_from_file(self, path):
         state = _load_state(path)

@@ -6,7 +6,10 @@ Replaces the master/worker split of the reference for the hot path:
 with members [r*P/N, (r+1)*P/N) evaluated on rank r. The exchange is one all-gather of the (P, 2)
 fitness (every rank then ranks the whole population identically) and one all-reduce (sum) of the
 D-float weighted noise sum; Adam then runs replicated, so theta needs no broadcast.
-On ROCm the 'nccl' backend is RCCL over xGMI.
+Two bindings of the exchange: torch.distributed (comm=None; on ROCm the 'nccl' backend is RCCL over
+xGMI, 'gloo' on CPU), or the engine's own C-ABI RCCL communicator (comm='engine':
+nicnes_allgather_fitness / nicnes_allreduce_grad after Engine.comm_init), for callers that do not
+run torch.distributed.
 """
 import torch
 import torch.distributed as dist
@@ -14,7 +17,7 @@ import torch.distributed as dist
 
 class PopulationRunner:
     def __init__(self, engine, population, sigma, l2coeff=0.0, stepsize=1e-3, beta1=0.9, beta2=0.999,
-                 epsilon=1e-08, rank=0, world_size=1, group=None):
+                 epsilon=1e-08, rank=0, world_size=1, group=None, comm=None):
         assert population % world_size == 0, 'population must split evenly over ranks'
         self.e = engine
         self.P = population
@@ -22,6 +25,9 @@ class PopulationRunner:
         self.l2coeff, self.stepsize, self.beta1, self.beta2, self.epsilon = l2coeff, stepsize, beta1, beta2, epsilon
         self.rank, self.world = rank, world_size
         self.group = group
+        if comm not in (None, 'engine'):
+            raise ValueError("comm: None (torch.distributed) or 'engine' (the engine's RCCL communicator)")
+        self.comm = comm
         self.local = population // world_size
         self.m0 = rank * self.local
         dev = engine.device
@@ -36,8 +42,19 @@ class PopulationRunner:
 
     def exchange_fitness(self):
         if self.world > 1:
-            dist.all_gather_into_tensor(self.fit_all, self.fit_local, group=self.group)
+            if self.comm == 'engine':
+                self.e.allgather_fitness(self.fit_local, self.fit_all)
+            else:
+                dist.all_gather_into_tensor(self.fit_all, self.fit_local, group=self.group)
         return self.fit_all
+
+    def reduce_noise_sum(self):
+        if self.world > 1:
+            if self.comm == 'engine':
+                self.e.allreduce_grad(self.gsum)
+            else:
+                dist.all_reduce(self.gsum, op=dist.ReduceOp.SUM, group=self.group)
+        return self.gsum
 
     def update(self, iteration, sync=True):
         """ranks -> weighted noise sum (local members) -> all-reduce -> Adam. Returns the update ratio
@@ -45,8 +62,7 @@ class PopulationRunner:
         _, w = self.e.rank_weights(self.fit_all)
         self.e.grad_partial(iteration, self.m0, self.local, w[self.m0:self.m0 + self.local], self.sigma,
                             out=self.gsum)
-        if self.world > 1:
-            dist.all_reduce(self.gsum, op=dist.ReduceOp.SUM, group=self.group)
+        self.reduce_noise_sum()
         return self.e.adam_step(self.gsum, self.P, self.l2coeff, self.stepsize, self.beta1, self.beta2,
                                 self.epsilon, sync=sync)
 

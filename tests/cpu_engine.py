@@ -56,6 +56,7 @@ class OracleEngine:
     def sgd_step(self, gsum, P, l2coeff, stepsize, momentum=0.9):
         if self.adam is None:
             self.adam = O.SGDOracle(self.theta_src.copy(), stepsize, momentum)
+        self.adam.stepsize, self.adam.momentum = stepsize, momentum      # a schedule may change them
         g = gsum.numpy().astype(np.float32) / np.float32(2 * P)
         ratio, theta = O.master_update(self.adam, g, l2coeff)
         self.theta32 = np.asarray(theta).astype(np.float32)
@@ -93,6 +94,7 @@ class OracleEngine:
     def adam_step(self, gsum, P, l2coeff, stepsize, beta1=0.9, beta2=0.999, epsilon=1e-08, sync=True):
         if self.adam is None:
             self.adam = O.AdamOracle(self.theta_src.copy(), stepsize, beta1, beta2, epsilon)
+        self.adam.stepsize = stepsize                                      # stepsize_divisor changes it
         g = gsum.numpy().astype(np.float32) / np.float32(2 * P)
         ratio, theta = O.master_update(self.adam, g, l2coeff)
         self.theta32 = np.asarray(theta).astype(np.float32)

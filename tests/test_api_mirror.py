@@ -259,3 +259,99 @@ def test_schedule_curriculum():
     # iteration.py:184-187: reached at it >= start and (it - start) % limit == 0 -> it = 2, 5, 8
     assert hits == [False, True, False, False, True, False, False, True]
     assert s.noise_stdev == 0.1 / 8 and s.batch_size == 64 and s.nb_samples_used == 8 + 8 + 16 * 3 + 32 * 3
+
+
+class _Loader:
+    """get_batch(split, batch_size) over a pool of images (the data.CocoFcDataLoader surface)."""
+
+    def __init__(self, fc, gts):
+        self.fc, self.gts, self.pos, self.sizes = fc, gts, 0, []
+
+    def get_batch(self, split, batch_size=None):
+        self.sizes.append(batch_size)
+        ix = [(self.pos + k) % len(self.gts) for k in range(batch_size)]
+        self.pos += batch_size
+        return {'fc_feats': np.repeat(self.fc[ix], 5, axis=0), 'gts': [self.gts[i] for i in ix]}
+
+
+def _sched_spec(P, bs, **cfg):
+    base = {'noise_stdev': 0.05, 'batch_size': bs, 'l2coeff': 1e-3, 'snapshot_freq': 0}
+    base.update(cfg)
+    return C.ExperimentSpec(_exp(nb_offspring=P, config=base, policy_options={'net': 'fc_caption', 'fitness': 'greedy'},
+                                 optimizer_options={'type': 'adam', 'args': {'stepsize': 0.01}}), vocab_size=63)
+
+
+def test_curriculum_draws_batches_at_the_scheduled_size():
+    """bs_multiplier (tools/iteration.py:149-153): with a loader the master asks for batches of the
+    scheduled size, so a batch-size curriculum changes what is evaluated; stepsize_divisor applies."""
+    dims, theta, fc, gts, df, n, table = tiny_workload(B=8)
+    spec = _sched_spec(2, 2, schedule_start=1, schedule_limit=2, bs_multiplier=2, stepsize_divisor=4)
+    eng = OracleEngine(dims, theta, fc, gts, df, n, table)
+    seen = []
+    orig = eng.set_batch
+    eng.set_batch = lambda f, g: (seen.append(len(g)), orig(f, g))
+    loader = _Loader(fc, gts)
+    m = M.EngineMaster(spec, eng)
+    m.run(loader, max_iterations=4)
+    # schedule reached at it = 1 and 3: the batch doubles after each
+    assert loader.sizes == [2, 4, 4, 8] and seen == [2, 4, 4, 8]
+    assert [r['batch_size'] for r in m.stats] == [4, 4, 8, 8]
+    assert m.opt.stepsize == 0.01 / 16
+
+
+def test_dispatched_loop_applies_the_schedule(workload, tmp_path):
+    """run_dispatched divides the step size when the schedule is reached, as run() and
+    the reference master (nic_nes_master.py:139-141) do; both loops end on the same theta."""
+    dims, theta, fc, gts, df, n, table = workload
+    P, iters = 4, 3
+    batch = {'fc_feats': fc, 'gts': gts}
+    cfg = dict(schedule_start=1, schedule_limit=2, stepsize_divisor=2)
+    local = M.EngineMaster(_sched_spec(P, 4, **cfg), _engine(workload), log_dir=str(tmp_path / 'a'))
+    local.run([batch] * iters, max_iterations=iters)
+    master = M.EngineMaster(_sched_spec(P, 4, **cfg), _engine(workload), log_dir=str(tmp_path / 'b'))
+    store = T.LocalStore()
+    worker = N.EngineWorker(_engine(workload), _sched_spec(P, 4, **cfg), worker_id=1)
+    th = threading.Thread(target=M.run_worker, args=(T.WorkerClient(store), worker),
+                          kwargs=dict(chunk=4, max_tasks=iters), daemon=True)
+    th.start()
+    master.run_dispatched(T.MasterClient(store), [batch] * iters, max_iterations=iters, result_timeout=120)
+    th.join(timeout=120)
+    assert local.opt.stepsize == master.opt.stepsize == 0.01 / 4
+    assert np.array_equal(local.e.theta()[0].numpy(), master.e.theta()[0].numpy())
+
+
+def test_run_ends_on_an_exhausted_iterator(workload):
+    """a one-shot iterator shorter than max_iterations ends the run instead of spinning."""
+    import itertools
+    dims, theta, fc, gts, df, n, table = workload
+    m = M.EngineMaster(_spec(2), _engine(workload))
+    stats = m.run(itertools.islice(iter([{'fc_feats': fc, 'gts': gts}] * 5), 2), max_iterations=5)
+    assert len(stats) == 2 and m.sched.iteration == 2
+
+
+def test_optimizer_file_is_reference_typed(workload, tmp_path):
+    """optimizer.tar stores m, v as fp64 numpy arrays, the reference's types
+    (optimizers.py:85-95)."""
+    import pickle
+    m = M.EngineMaster(_spec(2), _engine(workload), log_dir=str(tmp_path))
+    m.run([{'fc_feats': workload[2], 'gts': workload[3]}], max_iterations=1)
+    m.save_snapshot()
+    # weights_only load with the numpy allowlist (what _load_state does): arrays come back as ndarrays
+    import numpy.core.multiarray as ma
+    with torch.serialization.safe_globals([ma._reconstruct, np.ndarray, np.dtype, type(np.dtype(np.float64))]):
+        st = torch.load(str(tmp_path / 'snapshot' / 'optimizer.tar'), weights_only=True)
+    assert isinstance(st['m'], np.ndarray) and st['m'].dtype == np.float64 and isinstance(st['v'], np.ndarray)
+    assert pickle is not None
+
+
+def test_set_batch_not_skipped_when_an_id_is_reused(workload):
+    """A new batch whose dict reuses the id() of the freed previous one must still be loaded."""
+    dims, theta, fc, gts, df, n, table = workload
+    e = _engine(workload)
+    loads = []
+    orig = e.set_batch
+    e.set_batch = lambda f, g: (loads.append(f.shape[0]), orig(f, g))
+    m = M.EngineMaster(_spec(2), e)
+    for k in range(3):
+        m._set_batch({'fc_feats': fc[:k + 1], 'gts': gts[:k + 1]})       # each dict freed right after
+    assert loads == [1, 2, 3]

@@ -50,3 +50,41 @@ def test_two_rank_gloo_matches_single_rank(tmp_path):
     # both ranks hold the identical replicated theta
     a, b = np.load(tmp_path / 'r0_w2.npz'), np.load(tmp_path / 'r1_w2.npz')
     assert np.array_equal(a['theta'], b['theta'])
+
+
+def _run_master(rank, world, port, out_dir):
+    """EngineMaster.run (the NESMaster.run_master loop, nic_nes_master.py:56-168) sharded over gloo
+    ranks, with a noise / step-size schedule reached mid-run."""
+    from nicnes import config as C
+    from nicnes import master as M
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    if world > 1:
+        dist.init_process_group('gloo', rank=rank, world_size=world)
+    dims, theta, fc, gts, df, n, table = tiny_workload()
+    eng = OracleEngine(dims, theta, fc, gts, df, n, table)
+    exp = {'algorithm': 'nic_nes', 'nb_offspring': P,
+           'config': {'noise_stdev': SIGMA, 'batch_size': 4, 'l2coeff': 1e-3, 'snapshot_freq': 0,
+                      'schedule_start': 1, 'schedule_limit': 2, 'stdev_divisor': 2, 'stepsize_divisor': 2},
+           'policy_options': {'net': 'fc_caption', 'fitness': 'greedy', 'model_options': {}},
+           'optimizer_options': {'type': 'adam', 'args': {'stepsize': 1e-2}}}
+    spec = C.ExperimentSpec(exp, vocab_size=63)
+    m = M.EngineMaster(spec, eng, log_dir=os.path.join(out_dir, 'log%d' % rank), rank=rank, world_size=world)
+    m.run([{'fc_feats': fc, 'gts': gts}] * 3, max_iterations=3)
+    np.savez(os.path.join(out_dir, 'm%d_w%d.npz' % (rank, world)), theta=eng.theta32,
+             scores=np.array([r['score_mean'] for r in m.stats]), sigma=np.array([r['noise_stdev'] for r in m.stats]),
+             stepsize=np.float64(m.opt.stepsize))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def test_two_rank_engine_master_run_matches_single_rank(tmp_path):
+    _run_master(0, 1, _free_port(), str(tmp_path))
+    mp.spawn(_run_master, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    one = np.load(tmp_path / 'm0_w1.npz')
+    for rank in range(2):
+        two = np.load(tmp_path / ('m%d_w2.npz' % rank))
+        assert np.array_equal(one['scores'], two['scores']) and np.array_equal(one['sigma'], two['sigma'])
+        assert float(two['stepsize']) == float(one['stepsize']) == 1e-2 / 4
+        assert np.allclose(one['theta'], two['theta'], rtol=0, atol=1e-6)
+    assert np.array_equal(np.load(tmp_path / 'm0_w2.npz')['theta'], np.load(tmp_path / 'm1_w2.npz')['theta'])
