@@ -64,9 +64,33 @@ def logit_noise_bytes_per_member(V1=9488, R=128):
     return V1 * (R + 1) * 4
 
 
-def cpu_baseline(args, B):
-    """The reference CPU worker path (torch-CPU restatement, oracle/ref_worker.py) on this box's
-    host cores: one single-threaded process per core, one member per process."""
+def iteration_algorithmic_bytes(B, P, D=2865808):
+    """HBM bytes one iteration must move per GPU: every member's noise rows at each
+    decode step (step_noise_bytes_per_member), its noise slice once more for the weighted sum, the
+    weighted sum written once, and Adam's fp64 theta / m / v read + written with g read and theta32
+    written."""
+    return P * (step_noise_bytes_per_member(B) + 4 * D) + 4 * D + (3 * 2 * 8 + 4 + 4) * D
+
+
+PMC_FILES = {('nicnes_decode_step_kernel', 512, 128): 'profiles/r02_pmc_step_p512_b128.json',
+             ('nicnes_decode_logit_kernel<4>', 64, 128): 'profiles/r02_pmc_logit_p64_b128.json'}
+
+
+def load_pmc(kernel, P, B):
+    f = PMC_FILES.get((kernel, P, B))
+    if not f or not os.path.exists(os.path.join(REPO, f)):
+        return None
+    with open(os.path.join(REPO, f)) as fh:
+        rec = json.load(fh)
+    rec['file'] = f
+    return rec
+
+
+def cpu_baseline(args, B, P):
+    """The reference CPU path (torch-CPU restatement, oracle/ref_worker.py) on this box's host cores:
+    one single-threaded worker process per core -- the reference's cpu_count() - 2 workers (main.py:105),
+    capped by the CPUs this job may use -- at least one member each, then the master leg (ranks, fp32
+    weighted sum of the P noise vectors, Adam) at the full population P."""
     from oracle import ref_worker
     import nicnes.synthetic as S
     import torch
@@ -78,17 +102,31 @@ def cpu_baseline(args, B):
     with torch.no_grad():
         base, _ = m.sample(torch.from_numpy(fc))
     gts, df, ref_len_raw = S.build_references(base.numpy(), dims.vocab_size, 4321, 5, 4096, dims.T)
-    cores = max(1, min(args.cpu_cores, os.cpu_count() or 1))
+    node = os.cpu_count() or 1
+    usable = ref_worker.usable_cpus()
+    cores = args.cpu_cores or max(1, min(node - 2, usable))
     table = S.noise_table(1 << 24, 123)
     rng = np.random.default_rng(0)
     n_members = cores * args.cpu_members_per_core
-    deltas = [np.float32(args.sigma) * table[o: o + dims.D]
-              for o in (64 * rng.integers(0, (table.size - dims.D) // 64, n_members))]
-    rate, _, secs = ref_worker.time_members(theta, fc, gts, df, ref_len_raw, deltas, cores)
-    return {'value': round(rate, 4), 'unit': 'members/s', 'cores': cores, 'kind': 'port',
-            'sample': '%d members (2 rollouts of %d rows = %d unique images x5, 18+18 steps, pure-Python '
-                      'CIDEr-D), one single-threaded torch process per core; mean %.2f s/member'
-                      % (n_members, 5 * B, B, float(secs.mean()))}
+    offs = 64 * rng.integers(0, (table.size - dims.D) // 64, max(n_members, P))
+    deltas = [np.float32(args.sigma) * table[o: o + dims.D] for o in offs[:n_members]]
+    rate, fits, secs = ref_worker.time_members(theta, fc, gts, df, ref_len_raw, deltas, cores)
+    fit_P = np.resize(fits, (P, 2))          # the master's input: P fitness pairs (values recycled)
+    t_master, _ = ref_worker.time_master(fit_P, table, offs[:P], args.sigma, theta)
+    t_iter = P / rate + t_master
+    per_core = 1.0 / float(secs.mean())
+    return {'value': round(P / t_iter, 4), 'unit': 'members/s', 'cores': cores, 'kind': 'port',
+            'sample': '%d members (2 rollouts of %d rows = %d unique images x5, 18+18 steps, pure-Python CIDEr-D) '
+                      'on %d single-threaded worker processes (reference rule cpu_count()-2 = %d, capped by the '
+                      '%d CPUs this job may use); then the master leg at P = %d (ranks, fp32 weighted sum of the '
+                      'P noise vectors, fp64 Adam): %.2f s. Iteration = P / worker rate + master leg.'
+                      % (n_members, 5 * B, B, cores, node - 2, usable, P, t_master),
+            'worker_members_per_s': round(rate, 4), 'master_leg_s': round(t_master, 3),
+            'mean_s_per_member_per_core': round(float(secs.mean()), 3),
+            'node_cpus': node,
+            'node_projection_members_per_s': round(P / (P / (per_core * max(node - 2, 1)) + t_master), 4),
+            'node_projection_note': 'the reference rule cpu_count()-2 on every host CPU at the measured per-core '
+                                    'rate (linear, an upper bound for the reference)'}
 
 
 def main():
@@ -106,7 +144,7 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--decode-split', type=int, default=0, help='force S logit workgroups per member (0 = auto)')
     ap.add_argument('--decode-rows', type=int, default=0, help='force 4 (128-row) or 2 (64-row) slabs (0 = auto)')
-    ap.add_argument('--cpu-cores', type=int, default=16)
+    ap.add_argument('--cpu-cores', type=int, default=0, help='worker processes (0: cpu_count()-2 capped by the usable CPUs)')
     ap.add_argument('--cpu-members-per-core', type=int, default=1)
     args = ap.parse_args()
 
@@ -118,7 +156,7 @@ def main():
     # CPU leg first, before this process touches the GPU (its pool forks)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, B)
+        cpu = cpu_baseline(args, B, args.pop_per_gpu)
 
     import torch
     import torch.distributed as dist
@@ -190,13 +228,12 @@ def main():
         step_flop = logit_flops_per_member(B) * P_local / n_step
         alg_bytes = logit_noise_bytes_per_member() * P_local / n_step
     achieved = step_flop / (step_ms / 1e3) / 1e12
-    traffic = None
-    pmc = os.path.join(REPO, 'profiles', 'r01_decode_pmc.json')
-    if os.path.exists(pmc) and kname == 'nicnes_decode_step_kernel' and P_local == 512 and B == 128:
-        with open(pmc) as f:
-            rec = json.load(f)
-        if rec.get('kernel') == kname:
-            traffic = rec.get('hbm_bytes_per_launch')
+    # counter figures of the same kernel and workload from the committed rocprofv3 PMC profile
+    # (a profile-derived constant: PMC passes cannot run inside the timed bench process)
+    pmc = load_pmc(kname, P_local, B)
+    traffic = pmc['derived'].get('hbm_bytes_per_launch') if pmc else None
+    hbm_peak_bytes = HBM_PEAK_GBS * 1e9 * step_ms / 1e3
+    iter_bytes = iteration_algorithmic_bytes(B, P_local)
     out = {
         'metric': METRIC, 'value': round(value, 3), 'unit': 'members/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3), 'higher_is_better': True,
@@ -207,8 +244,10 @@ def main():
                                % (P, P_local, B, args.sigma) + (", 'bu' fc features" if args.bu else '')
                                + (', fitness %s' % args.fitness if args.fitness != 'greedy' else ''),
                    'population': P, 'members_per_gpu': P_local, 'batch_size': B, 'seq_length': 16,
-                   'vocab_size': 9487, 'parallelism': 'population-sharded x%d, RCCL all-gather + all-reduce'
-                   % world},
+                   'vocab_size': 9487,
+                   'parallelism': ('none (one GPU, no collective)' if world == 1 else
+                                   'population-sharded x%d, %s all-gather of fitness + all-reduce of the noise sum'
+                                   % (world, 'RCCL' if backend == 'nccl' else backend))},
         'roofline': {'bound': 'mfma', 'kernel': kname, 'achieved': round(achieved, 3),
                      'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                      'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,
@@ -216,6 +255,14 @@ def main():
                      'algorithmic_flop_per_launch': step_flop,
                      'algorithmic_bytes_per_launch': alg_bytes,
                      'traffic_over_algorithmic': (round(traffic / alg_bytes, 3) if traffic else None),
+                     'traffic_source': pmc['file'] if pmc else None,
+                     'hbm_frac': round(alg_bytes / hbm_peak_bytes, 4),
+                     'hbm_frac_counters': round(traffic / hbm_peak_bytes, 4) if traffic else None,
+                     'mfma_busy': round(pmc['derived']['mfma_busy'], 4) if pmc and 'mfma_busy' in pmc['derived'] else None,
+                     'valu_insts_per_mfma': (round(pmc['derived']['valu_insts_per_mfma'], 3)
+                                             if pmc and 'valu_insts_per_mfma' in pmc['derived'] else None),
+                     'iteration_hbm_frac': round(iter_bytes * args.steps / dt / 1e9 / HBM_PEAK_GBS, 4),
+                     'iteration_algorithmic_bytes': iter_bytes,
                      'decode': {'ms_per_step': round(dec_s * 1e3, 3), 'algorithmic_flop': flops,
                                 'tflops': round(flops / dec_s / 1e12, 3),
                                 'frac': round(flops / dec_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),

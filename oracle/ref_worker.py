@@ -11,7 +11,10 @@ population member, on the GPU box's host cores (the reference itself cannot trav
                          steps; fc rows duplicated seq_per_img = 5 times (dataloader.py:175)
       compute_ciders     policies.py:145-193 with the pure-Python CIDEr-D of oracle/cider_ref.py
     theta - delta, rollout again
-One single-threaded process per core, as src/main.py:8-11,144-153 runs workers.
+One single-threaded process per core, as src/main.py:8-11,144-153 runs workers; then the master leg
+(time_master): NESMaster.gradient_estimate -- compute_centered_ranks, batched_weighted_sum in fp32
+np.dot groups of 500 -- and Adam.update in fp64 numpy (nic_nes_master.py:123-137,170-221,
+optimizers.py:15-22,78-83) over the P received noise vectors.
 """
 import os
 import time
@@ -145,3 +148,58 @@ def time_members(theta32, fc_unique, gts, df, ref_len_raw, deltas, processes):
 
 def _noop(_):
     return os.getpid()
+
+
+def usable_cpus():
+    """CPUs this process may run on: the cgroup v2 quota when one is set (a GPU box shares its host),
+    else the affinity mask."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    try:
+        quota, period = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if quota != 'max':
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _centered_ranks(x):
+    """compute_centered_ranks / compute_ranks (nic_nes_master.py:184-205): default argsort as the
+    reference calls it"""
+    r = np.empty(x.size, dtype=int)
+    r[x.ravel().argsort()] = np.arange(x.size)
+    y = r.reshape(x.shape).astype(np.float64)
+    y /= (x.size - 1)
+    y -= .5
+    return y
+
+
+def time_master(fitness, table, indices, sigma, theta32, l2coeff=1e-7, stepsize=1e-3):
+    """The reference master's per-iteration leg over P results, timed: ranks, the fp32 weighted sum
+    of the P noise vectors in groups of 500 (batched_weighted_sum), /2F, then Adam in fp64 numpy.
+    The noise vectors are materialised first, as the master holds the received arrays (not timed).
+    Returns (seconds, gradient)."""
+    D = theta32.size
+    s = np.float32(sigma)
+    vecs = np.empty((len(indices), D), np.float32)
+    for i, idx in enumerate(indices):
+        np.multiply(s, table[idx: idx + D], out=vecs[i])
+    theta = theta32.copy()
+    m = np.zeros(D, np.float64)
+    v = np.zeros(D, np.float64)
+    t0 = time.perf_counter()
+    cr = _centered_ranks(np.asarray(fitness, np.float64))
+    w = cr[:, 0] - cr[:, 1]
+    total = 0.
+    for k in range(0, len(indices), 500):
+        total += np.dot(np.asarray(w[k:k + 500], dtype=np.float32), vecs[k:k + 500])
+    g = total / cr.size
+    globalg = -g + l2coeff * theta
+    a = stepsize * np.sqrt(1 - 0.999) / (1 - 0.9)
+    m = 0.9 * m + (1 - 0.9) * globalg
+    v = 0.999 * v + (1 - 0.999) * (globalg * globalg)
+    step = -a * m / (np.sqrt(v) + 1e-08)
+    _ = np.linalg.norm(step) / np.linalg.norm(theta)
+    theta = theta + step
+    secs = time.perf_counter() - t0
+    return secs, g

@@ -15,7 +15,8 @@ import os
 
 
 def grid_of(row):
-    return tuple(int(row.get(k, 0) or 0) for k in ('Grid_Size_X', 'Grid_Size_Y', 'Grid_Size_Z', 'Grid_Size'))
+    x, y, z = (int(row.get(k, 1) or 1) for k in ('Grid_Size_X', 'Grid_Size_Y', 'Grid_Size_Z'))
+    return (x * y * z, x, y, z)          # the largest total grid first (a split launch has a wide x)
 
 
 def main():
@@ -33,7 +34,7 @@ def main():
         with open(fn) as f:
             for row in csv.DictReader(f):
                 name = row['Kernel_Name'].split('(')[0]
-                if not name.startswith(a.prefix):
+                if a.prefix not in name:
                     continue
                 dur = (int(row['End_Timestamp']) - int(row['Start_Timestamp'])) / 1e6
                 launches.setdefault(name, []).append((int(row['Dispatch_Id']), grid_of(row), dur))
