@@ -90,6 +90,13 @@ int nicnes_noise_indices(nicnes_handle* h, uint64_t iteration, int32_t member_be
 int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
                     double* fitness_out, int32_t* seq_out, void* stream);
 
+/* The perturbations themselves, delta_k = fp32(sigma * table[idx_k : idx_k + D]) for members
+ * [member_begin, +count): out [count, D] fp32. What PolicyNet.evolve returns
+ * (src/algorithm/nets.py:101-102, 118) and NESResult.evolve_noise carries to an unchanged reference
+ * master (src/algorithm/nic_nes/nic_nes_worker.py:156-161); the engine's own master never needs them. */
+int nicnes_noise_vectors(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
+                         float* out, void* stream);
+
 /* Fitness criterion (Fitness enum + get_criterium, src/captioning/policies.py:22-61, applied at
  * :119-125): GREEDY = 100 * mean CIDEr-D; the greedy_* modes weight each step's probability of the
  * greedy token by the row's CIDEr-D (src/captioning/fitness.py:43-132). Other modes (sample,

@@ -478,6 +478,19 @@ int nicnes_noise_indices(nicnes_handle* h, uint64_t iteration, int32_t member_be
     return NICNES_OK;
 }
 
+int nicnes_noise_vectors(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
+                         float* out, void* stream) {
+    if (!h || !out || member_begin < 0 || count < 1) return NICNES_ERR_INVALID;
+    if (count > h->cfg.max_members) return fail(h, NICNES_ERR_INVALID, "count > max_members");
+    if (!h->noise) return fail(h, NICNES_ERR_INVALID, "nicnes_set_noise_table first");
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, nicnes_launch_noise_index(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, h->cfg.noise_len,
+                                      (uint64_t)h->D, h->nidx, s));
+    HIPC(h, nicnes_launch_noise_vectors(h->noise, h->nidx, count, h->D, sigma, out, s));
+    return NICNES_OK;
+}
+
 int nicnes_set_fitness_mode(nicnes_handle* h, int32_t mode) {
     if (!h) return NICNES_ERR_INVALID;
     if (mode < NICNES_FITNESS_GREEDY || mode > NICNES_FITNESS_GREEDY_AVGPROB)

@@ -192,6 +192,24 @@ extern "C" hipError_t nicnes_launch_grad(const float* noise, const uint64_t* idx
     return hipGetLastError();
 }
 
+// delta_k = fp32(sigma * z[idx_k + j]) for k < count, j < dim: the vectors PolicyNet.evolve returns
+// (src/algorithm/nets.py:101-102) rebuilt from the table, for the reference-format NESResult
+// (nic_nes_worker.py:156-161). Coalesced over j, one row of the grid per member.
+__global__ __launch_bounds__(256) void nicnes_noise_vectors_kernel(const float* noise, const uint64_t* idx, int64_t dim,
+                                                                   float sigma, float* out) {
+    const int k = blockIdx.y;
+    const float* z = noise + idx[k];
+    float* o = out + (size_t)k * dim;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < dim; j += (int64_t)gridDim.x * blockDim.x)
+        o[j] = sigma * z[j];
+}
+
+extern "C" hipError_t nicnes_launch_noise_vectors(const float* noise, const uint64_t* idx, int count, int64_t dim,
+                                                  float sigma, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(nicnes_noise_vectors_kernel, dim3(512, count), dim3(256), 0, s, noise, idx, dim, sigma, out);
+    return hipGetLastError();
+}
+
 extern "C" int nicnes_adam_blocks(int64_t dim) { return (int)((dim + 255) / 256); }
 
 extern "C" hipError_t nicnes_launch_adam(const AdamParams* p, double* norms_out, hipStream_t s) {

@@ -157,6 +157,15 @@ class Engine:
                                               self._stream()), self.h, 'noise_indices')
         return out
 
+    def noise_vectors(self, iteration, member_begin, count, sigma, out=None):
+        """delta [count, D] fp32 = fp32(sigma * table slice) of members [member_begin, +count) (the
+        vectors a reference-format NESResult carries)."""
+        o = out if out is not None else torch.empty((count, self.D), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_noise_vectors(self.h, ctypes.c_uint64(iteration), member_begin, count,
+                                              ctypes.c_float(sigma), _ptr(o), self._stream()), self.h, 'noise_vectors')
+        return o
+
     # Fitness enum values the engine implements (src/captioning/policies.py:22-35) -> nicnes.h codes
     FITNESS_MODES = {'greedy': 0, 'greedy_logprob': 1, 'greedy_expprob': 2, 'greedy_linprob': 3,
                      'greedy_avgprob': 4}

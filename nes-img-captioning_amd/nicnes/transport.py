@@ -194,12 +194,125 @@ class LocalStore:
         return _Pipeline(self)
 
 
+class _SeqPipeline:
+    """pipeline() of stores without transactions: the queued commands run in order on execute()."""
+
+    def __init__(self, store):
+        self.s, self.ops = store, []
+
+    def __getattr__(self, name):
+        fn = getattr(self.s, name)
+
+        def queue(*a, **k):
+            self.ops.append((fn, a, k))
+            return self
+        return queue
+
+    def watch(self, *keys):
+        return None
+
+    def multi(self):
+        return None
+
+    def execute(self):
+        out = [fn(*a, **k) for fn, a, k in self.ops]
+        self.ops = []
+        return out
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.ops = []
+        return False
+
+
+class TCPStoreRedis:
+    """The same redis subset over torch.distributed.TCPStore, for master and workers in separate
+    processes when no redis server exists (this image has none): 'tcp://host:port' in connect().
+    mset writes one snapshot key besides the keys, and mget of keys that snapshot holds reads it, so
+    a worker never pairs a new task id with old task data. Lists are TCPStore queues."""
+
+    _SNAP = '__nicnes_mset__'
+
+    def __init__(self, host, port, is_master=False, timeout=60.0):
+        from datetime import timedelta
+        import torch.distributed as dist
+        self.host, self.port = host, int(port)
+        self.s = dist.TCPStore(host, self.port, is_master=is_master, wait_for_workers=False,
+                               timeout=timedelta(seconds=timeout))
+
+    def ping(self):
+        return True
+
+    def set(self, k, v):
+        self.s.set(k, v if isinstance(v, bytes) else str(v).encode())
+        return True
+
+    def get(self, k):
+        return self.s.get(k) if self.s.check([k]) else None
+
+    def mset(self, mapping):
+        vals = {k: (v if isinstance(v, bytes) else str(v).encode()) for k, v in mapping.items()}
+        for k, v in vals.items():
+            self.s.set(k, v)
+        self.s.set(self._SNAP, msgpack.packb(vals, use_bin_type=True))
+        return True
+
+    def mget(self, keys):
+        snap = self.get(self._SNAP)
+        if snap is not None:
+            d = msgpack.unpackb(snap, raw=False)
+            if all(k in d for k in keys):
+                return [d[k] for k in keys]
+        return [self.get(k) for k in keys]
+
+    def delete(self, *keys):
+        return sum(int(self.s.delete_key(k)) for k in keys)
+
+    def incrby(self, k, n=1):
+        return int(self.s.add(k, int(n)))
+
+    def rpush(self, k, *vals):
+        for v in vals:
+            self.s.queue_push(k, v)
+        return int(self.s.queue_len(k))
+
+    def blpop(self, k, timeout=0):
+        deadline = None if not timeout else time.monotonic() + timeout
+        while self.s.queue_len(k) == 0:
+            if deadline is not None and time.monotonic() >= deadline:
+                return None
+            time.sleep(0.002)
+        return (k, self.s.queue_pop(k, False))
+
+    def llen(self, k):
+        return int(self.s.queue_len(k))
+
+    def ltrim(self, k, start, end):
+        if (start, end) != (-1, -1):
+            raise NotImplementedError('TCPStoreRedis.ltrim keeps only the newest item (flush_results)')
+        while self.s.queue_len(k) > 1:
+            self.s.queue_pop(k, False)
+        return True
+
+    def publish(self, channel, msg):
+        return 0
+
+    def pipeline(self):
+        return _SeqPipeline(self)
+
+
 def connect(cfg):
-    """LocalStore / redis-like object -> itself; dict -> redis.StrictRedis(**cfg) (needs redis-py)."""
+    """LocalStore / redis-like object -> itself; 'tcp://host:port' -> TCPStoreRedis (client);
+    dict -> redis.StrictRedis(**cfg) (needs redis-py)."""
     if cfg is None:
         return LocalStore()
     if hasattr(cfg, 'rpush'):
         return cfg
+    if isinstance(cfg, str) and cfg.startswith('tcp://'):
+        host, port = cfg[len('tcp://'):].rsplit(':', 1)
+        return TCPStoreRedis(host, int(port))
     try:
         import redis
     except ImportError as e:   # pragma: no cover - redis-py is absent from this image
@@ -224,21 +337,31 @@ def _retry_get(store, key, tries=300, delay=0.05):
 
 
 # ---------------------------------------------------------------- clients -------------------------
+class MsgpackCodec:
+    """The engine's own wire: msgpack with an ndarray extension (plain data only)."""
+    name = 'msgpack'
+    serialize = staticmethod(serialize)
+    deserialize = staticmethod(deserialize)
+
+
 class MasterClient:
-    def __init__(self, master_redis_cfg=None):
+    """codec: MsgpackCodec (default) or nicnes.refwire.RefPickleCodec (the reference's pickle wire)."""
+
+    def __init__(self, master_redis_cfg=None, codec=None):
         self.task_counter = 0
         self.master_redis = connect(master_redis_cfg)
+        self.codec = codec or MsgpackCodec
 
     def declare_experiment(self, exp):
-        self.master_redis.set(EXP_KEY, serialize(exp))
+        self.master_redis.set(EXP_KEY, self.codec.serialize(exp))
 
     def declare_task(self, task_data):
         task_id = self.task_counter
         self.task_counter += 1
-        data = serialize(task_data)
+        data = self.codec.serialize(task_data)
         (self.master_redis.pipeline()
          .mset({TASK_ID_KEY: task_id, TASK_DATA_KEY: data, MEMBER_KEY + ':%d' % task_id: 0})
-         .publish(TASK_CHANNEL, serialize((task_id, data)))
+         .publish(TASK_CHANNEL, self.codec.serialize((task_id, data)))
          .execute())
         return task_id
 
@@ -246,7 +369,7 @@ class MasterClient:
         item = self.master_redis.blpop(RESULTS_KEY, timeout=timeout)
         if item is None:
             return None, None
-        task_id, result = deserialize(item[1])
+        task_id, result = self.codec.deserialize(item[1])
         return task_id, result
 
     def flush_results(self):
@@ -256,20 +379,21 @@ class MasterClient:
 class WorkerClient:
     """Argument order as in dist.py:162 (relay, master); with one store both are the same."""
 
-    def __init__(self, relay_redis_cfg=None, master_redis_cfg=None):
+    def __init__(self, relay_redis_cfg=None, master_redis_cfg=None, codec=None):
         self.local_redis = connect(relay_redis_cfg)
         self.master_redis = self.local_redis if master_redis_cfg is None else connect(master_redis_cfg)
         self.cached_task_id, self.cached_task_data = None, None
+        self.codec = codec or MsgpackCodec
 
     def get_experiment(self):
-        return deserialize(_retry_get(self.local_redis, EXP_KEY))
+        return self.codec.deserialize(_retry_get(self.local_redis, EXP_KEY))
 
     def get_current_task(self):
         task_id = int(_retry_get(self.local_redis, TASK_ID_KEY))
         if task_id != self.cached_task_id:
             tid, data = self.local_redis.mget([TASK_ID_KEY, TASK_DATA_KEY])
             if int(tid) == task_id:
-                self.cached_task_id, self.cached_task_data = task_id, deserialize(data)
+                self.cached_task_id, self.cached_task_data = task_id, self.codec.deserialize(data)
         return self.cached_task_id, self.cached_task_data
 
     def claim_members(self, task_id, count):
@@ -278,8 +402,8 @@ class WorkerClient:
         return end - count
 
     def push_result(self, task_id, result):
-        self.local_redis.rpush(RESULTS_KEY, serialize((task_id, result)))
+        self.local_redis.rpush(RESULTS_KEY, self.codec.serialize((task_id, result)))
 
     def push_results(self, task_id, results):
         if results:
-            self.local_redis.rpush(RESULTS_KEY, *[serialize((task_id, r)) for r in results])
+            self.local_redis.rpush(RESULTS_KEY, *[self.codec.serialize((task_id, r)) for r in results])

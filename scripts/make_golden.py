@@ -28,6 +28,11 @@ Fixtures (all .npz, loadable with allow_pickle=False):
                                   (nic_nes_master.py:170-221) imported with placeholder redis/torchvision
                                   modules: P = 512 tie-free fitness and a tied one, and the fp32 gradient
                                   of 512 table-noise vectors on 4096 sampled coordinates
+  wire_reference.npz              the reference's wire bytes: dist.serialize (src/dist.py:25-26, pickle
+                                  protocol -1) of an NESTask (nic_nes_master.py:27-28) as the master declares
+                                  it (a batch dict of numpy arrays / lists / dicts), of (task_id, NESResult) as
+                                  a worker pushes it (nic_nes_worker.py:156-161, dist.py:199-201), and of an
+                                  experiment dict (dist.py:73-76)
   fitness_criteria.npz            the greedy_* fitness criteria (src/captioning/fitness.py:43-132, chosen
                                   by Fitness.get_criterium, src/captioning/policies.py:50-61) on seeded
                                   logprobs / sequences / per-row CIDEr rewards, as CaptPolicy.rollout
@@ -196,6 +201,44 @@ def master_ranks_grad_fixture():
     print('master: grad dtype', np.asarray(g).dtype, 'max|g|', float(np.abs(g).max()))
 
 
+def wire_fixture():
+    for name in ('redis', 'torchvision'):
+        try:
+            __import__(name)
+        except ImportError:
+            sys.modules[name] = _Placeholder(name)
+    np.float = float
+    from algorithm.nic_nes.nic_nes_master import NESTask, NESResult   # reference wire types
+    from dist import serialize                                       # reference codec
+    rng = np.random.Generator(np.random.PCG64(21))
+    B, T = 3, 16
+    fc = rng.standard_normal((B * 5, 32)).astype(np.float32)
+    gts = [rng.integers(0, 50, (int(n), T)).astype(np.uint32) for n in (5, 6, 5)]
+    labels = np.zeros((B * 5, T + 2), dtype='int')
+    labels[:, 1:T + 1] = rng.integers(0, 50, (B * 5, T))
+    batch = {'fc_feats': fc, 'att_feats': np.zeros((B * 5, 1, 1), np.float32), 'labels': labels,
+             'masks': (labels > 0).astype(np.float32), 'att_masks': None, 'gts': gts,
+             'bounds': {'it_pos_now': 3, 'it_max': 113287, 'wrapped': False},
+             'infos': [{'ix': 7 * i, 'id': 1000 + i, 'file_path': 'train2014/COCO_%d.jpg' % i} for i in range(B)]}
+    task = NESTask(current='logs/nic_nes_mscoco_fc_caption_1/models/current/0_current_params.pth', batch_data=batch,
+                   noise_stdev=0.01, log_dir='logs/nic_nes_mscoco_fc_caption_1', ref_batch=None, batch_size=B)
+    D = 1000
+    noise = (np.float32(0.01) * rng.standard_normal(D).astype(np.float32))
+    fitness = np.stack((71.25, 64.5))
+    result = NESResult(worker_id=3, evolve_noise=noise, fitness=fitness, mem_usage=123456789)
+    eval_result = NESResult(worker_id=4, eval_score=55.5, mem_usage=1234)
+    with open('/root/reference/experiments/mscoco_nes.json') as f:
+        exp = json.load(f)
+    np.savez_compressed(os.path.join(OUT, 'wire_reference.npz'),
+                        task_bytes=np.frombuffer(serialize(task), np.uint8),
+                        result_bytes=np.frombuffer(serialize((7, result)), np.uint8),
+                        eval_bytes=np.frombuffer(serialize((7, eval_result)), np.uint8),
+                        exp_bytes=np.frombuffer(serialize(exp), np.uint8),
+                        noise=noise, fitness=fitness, fc=fc, labels=labels,
+                        gts_flat=np.concatenate(gts), gts_rows=np.array([len(g) for g in gts]))
+    print('wire: task %d B, result %d B' % (len(serialize(task)), len(serialize((7, result)))))
+
+
 def perturb_fixture():
     d = O.Dims(vocab_size=63, E=32, R=32, F=64)
     model = ref_model(d)
@@ -320,6 +363,7 @@ def all_fixtures():
     fitness_criteria_fixture()
     decode_bench_fixture()
     master_ranks_grad_fixture()
+    wire_fixture()
 
 
 if __name__ == '__main__':

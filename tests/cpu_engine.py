@@ -46,6 +46,12 @@ class OracleEngine:
     def noise_indices(self, iteration, member_begin, count):
         return torch.tensor([self._idx(iteration, member_begin + k) for k in range(count)], dtype=torch.int64)
 
+    def noise_vectors(self, iteration, member_begin, count, sigma, out=None):
+        s = np.float32(sigma)
+        v = np.stack([s * self.table[self._idx(iteration, member_begin + k): self._idx(iteration, member_begin + k) + self.D]
+                      for k in range(count)])
+        return torch.from_numpy(v)
+
     def adam_state(self):
         if self.adam is None:
             z = torch.zeros(self.D, dtype=torch.float64)

@@ -1,0 +1,126 @@
+"""The GPU worker side of the drop-in boundary:
+* `python -m nicnes.worker` (one spawned process per GPU, the default engine factory: an Engine with
+  the shared table and the df file of --df_path) serving EngineMaster.run_dispatched in this process
+  over a TCPStore: two iterations give the theta of the local loop on the same inputs;
+* an engine worker on the reference's pickle wire: each result's fitness equals Engine.evaluate and
+  its evolve_noise equals fp32(sigma * table slice), the vector the reference master sums."""
+import os
+import signal
+import socket
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O          # noqa: E402
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NOISE_LEN = 1 << 23
+
+
+def _spec(P, bs):
+    from nicnes import config as C
+    return C.ExperimentSpec({'algorithm': 'nic_nes', 'nb_offspring': P,
+                             'config': {'noise_stdev': 0.01, 'batch_size': bs, 'l2coeff': 1e-7, 'snapshot_freq': 0},
+                             'policy_options': {'net': 'fc_caption', 'fitness': 'greedy', 'model_options': {}},
+                             'optimizer_options': {'type': 'adam', 'args': {'stepsize': 1e-3}}})
+
+
+def _workload(B=12):
+    import nicnes.synthetic as S
+    dims = O.Dims()
+    theta = O.make_theta(dims, 2, 4.0, 0.1)
+    fc = np.random.Generator(np.random.PCG64(77)).standard_normal((B, dims.F)).astype(np.float32)
+    base, _, _ = O.decode(dims, theta, fc)
+    gts, df, n = S.build_references(base, dims.vocab_size, seed=5, n_refs=5, df_sets=128)
+    return theta, fc, gts, df, n
+
+
+def _engine(P, B, df, n):
+    import nicnes
+    e = nicnes.Engine(max_batch=B, max_members=P, noise_len=NOISE_LEN, noise_seed=0)
+    e.set_noise_table(O.noise_table(NOISE_LEN, 123))
+    keys, vals = nicnes.df_table_arrays(df)
+    e.set_df_table(keys, vals, np.log(float(n)))
+    return e
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_worker_pool_process_serves_engine_master(tmp_path):
+    from nicnes import data, master as M, transport as T
+    from nicnes.worker import STOP_KEY
+    P, B = 8, 12
+    theta, fc, gts, df, n = _workload(B)
+    batch = {'fc_feats': fc, 'gts': gts}
+    e = _engine(P, B, df, n)
+    try:
+        local = M.EngineMaster(_spec(P, B), e, log_dir=str(tmp_path / 'a'), theta=theta)
+        local.run([batch] * 2, max_iterations=2)
+        want = e.theta()[0].cpu().numpy()
+        df_path = str(tmp_path / 'df.json')
+        data.save_df_table(df_path, df, n)
+        port = _free_port()
+        store = T.TCPStoreRedis('127.0.0.1', port, is_master=True)
+        env = dict(os.environ, PYTHONPATH=os.pathsep.join([REPO, os.path.join(REPO, 'nes-img-captioning_amd')]))
+        cmd = [sys.executable, '-m', 'nicnes.worker', '--store', 'tcp://127.0.0.1:%d' % port, '--num_workers', '1',
+               '--wire', 'engine', '--chunk', '4', '--noise_len', str(NOISE_LEN), '--noise_seed', '0',
+               '--df_path', df_path, '--check_interval', '0.5']
+        pool = subprocess.Popen(cmd, env=env, cwd=REPO, start_new_session=True, stdout=subprocess.DEVNULL,
+                                stderr=open(str(tmp_path / 'pool.log'), 'w'))
+        try:
+            e.set_theta(theta)
+            e.set_adam_state(np.zeros(e.D), np.zeros(e.D), 0)
+            master = M.EngineMaster(_spec(P, B), e, log_dir=str(tmp_path / 'b'))
+            master.run_dispatched(T.MasterClient(store), [batch] * 2, max_iterations=2, result_timeout=240)
+            assert np.array_equal(e.theta()[0].cpu().numpy(), want)
+            store.set(STOP_KEY, b'1')
+            assert pool.wait(timeout=120) == 0
+        finally:
+            if pool.poll() is None:
+                os.killpg(pool.pid, signal.SIGKILL)
+    finally:
+        e.close()
+
+
+def test_reference_wire_results_from_the_engine(tmp_path):
+    from nicnes import nes as N, refwire as W, transport as T
+    P, B = 4, 12
+    theta, fc, gts, df, n = _workload(B)
+    e = _engine(P, B, df, n)
+    try:
+        path = str(tmp_path / '0_current_params.pth')
+        torch.save(N.state_dict_from_vector(torch.from_numpy(theta), N.param_shapes(e)), path)
+        store = T.LocalStore()
+        mc = T.MasterClient(store, codec=W.RefPickleCodec)
+        mc.declare_experiment(_spec(P, B).exp)
+        batch = {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts}
+        tid = mc.declare_task(W.RefNESTask(current=path, batch_data=batch, noise_stdev=0.01, batch_size=B))
+        stop = threading.Event()
+        worker = N.EngineWorker(e, _spec(P, B), worker_id=5)
+        th = threading.Thread(target=W.run_reference_worker, daemon=True,
+                              args=(T.WorkerClient(store, codec=W.RefPickleCodec), worker),
+                              kwargs=dict(chunk=2, stop=stop, max_results=4))
+        th.start()
+        th.join(120)
+        got = [mc.pop_result(timeout=5) for _ in range(4)]
+        fit = e.evaluate(tid, 0, 4, 0.01).cpu().numpy()
+        table = O.noise_table(NOISE_LEN, 123)
+        for k, (t, r) in enumerate(got):
+            assert t == tid and np.array_equal(r.fitness, fit[k])
+            idx = O.noise_index(0, tid, k, NOISE_LEN, e.D)
+            assert np.array_equal(r.evolve_noise, np.float32(0.01) * table[idx: idx + e.D])
+    finally:
+        e.close()

@@ -1,0 +1,167 @@
+"""The drop-in worker side: the reference's pickle wire (nicnes.refwire) checked byte for byte
+against the reference's own dist.serialize output, an engine worker serving a reference-style
+master over it, and the `python -m nicnes.worker` pool (one process per device, spawned; a killed
+worker restarted as a fresh process) serving EngineMaster.run_dispatched across processes over a
+TCPStore. CPU only: the workers run the oracle engine (tests/worker_factory.py)."""
+import os
+import pickle
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from nicnes import config as C
+from nicnes import master as M
+from nicnes import nes as N
+from nicnes import refwire as W
+from nicnes import transport as T
+from oracle import oracle as O
+from tests.cpu_engine import OracleEngine, tiny_workload
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _wire(golden_dir):
+    return np.load(golden_dir + '/wire_reference.npz')
+
+
+def test_reference_task_decodes(golden_dir):
+    z = _wire(golden_dir)
+    task = W.loads(z['task_bytes'].tobytes())
+    assert isinstance(task, W.RefNESTask) and task.batch_size == 3 and task.noise_stdev == 0.01
+    bd = task.batch_data
+    assert np.array_equal(bd['fc_feats'], z['fc']) and np.array_equal(bd['labels'], z['labels'])
+    assert np.array_equal(np.concatenate(bd['gts']), z['gts_flat'])
+    assert [len(g) for g in bd['gts']] == list(z['gts_rows'])
+    assert bd['infos'][1]['id'] == 1001 and bd['att_masks'] is None
+    assert W.dumps(task) == z['task_bytes'].tobytes()          # re-encodes to the same bytes
+    exp = W.loads(z['exp_bytes'].tobytes())
+    assert exp['algorithm'] == 'nic_nes' and exp['policy_options']['net'] == 'fc_caption'
+    C.ExperimentSpec(exp)                                       # the engine accepts mscoco_nes.json as sent
+
+
+def test_engine_results_are_the_reference_bytes(golden_dir):
+    """What an engine worker pushes is byte-identical to what the reference worker pushes for the
+    same content, so the reference master's pickle.loads reads it with its own NESResult class."""
+    z = _wire(golden_dir)
+    res = W.RefNESResult(worker_id=3, evolve_noise=z['noise'], fitness=z['fitness'], mem_usage=123456789)
+    assert W.dumps((7, res)) == z['result_bytes'].tobytes()
+    ev = W.RefNESResult(worker_id=4, eval_score=55.5, mem_usage=1234)
+    assert W.dumps((7, ev)) == z['eval_bytes'].tobytes()
+    tid, back = W.loads(z['result_bytes'].tobytes())
+    assert tid == 7 and np.array_equal(back.evolve_noise, z['noise']) and np.array_equal(back.fitness, z['fitness'])
+
+
+def test_restricted_unpickler_refuses_code():
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ('true',))
+    with pytest.raises(pickle.UnpicklingError):
+        W.loads(pickle.dumps(Evil()))
+    with pytest.raises(pickle.UnpicklingError):
+        W.loads(pickle.dumps(torch.zeros(2)))
+
+
+def _spec(P, bs=4, **cfg):
+    c = {'noise_stdev': 0.05, 'batch_size': bs, 'l2coeff': 1e-3, 'snapshot_freq': 0}
+    c.update(cfg)
+    return C.ExperimentSpec({'algorithm': 'nic_nes', 'dataset': 'mscoco', 'nb_offspring': P, 'config': c,
+                             'policy_options': {'net': 'fc_caption', 'fitness': 'greedy', 'model_options': {}},
+                             'optimizer_options': {'type': 'adam', 'args': {'stepsize': 0.01}}}, vocab_size=63)
+
+
+@pytest.mark.parametrize('eval_prob', [0.0, 1.0])
+def test_reference_wire_worker_serves_a_reference_master(tmp_path, eval_prob):
+    dims, theta, fc, gts, df, n, table = tiny_workload()
+    eng = OracleEngine(dims, theta, fc, gts, df, n, table)
+    path = str(tmp_path / '0_current_params.pth')
+    torch.save(N.state_dict_from_vector(torch.from_numpy(theta), N.param_shapes(eng)), path)
+    store = T.LocalStore()
+    mc = T.MasterClient(store, codec=W.RefPickleCodec)           # plays the reference master
+    mc.declare_experiment(_spec(4).exp)
+    batch = {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts, 'labels': np.zeros((20, 18), dtype='int')}
+    tid = mc.declare_task(W.RefNESTask(current=path, batch_data=batch, noise_stdev=0.05, log_dir=str(tmp_path),
+                                       batch_size=4))
+    worker = N.EngineWorker(OracleEngine(dims, theta, fc, gts, df, n, table), _spec(4), worker_id=11)
+    stop = threading.Event()
+    th = threading.Thread(target=W.run_reference_worker, daemon=True,
+                          args=(T.WorkerClient(store, codec=W.RefPickleCodec), worker),
+                          kwargs=dict(chunk=2, eval_prob=eval_prob, seed=0, stop=stop))
+    th.start()
+    got = []
+    try:
+        while len(got) < 4:
+            t, r = mc.pop_result(timeout=60)
+            assert t is not None, 'no result within 60 s'
+            got.append((t, r))
+    finally:
+        stop.set()
+        th.join(60)
+    assert all(t == tid and isinstance(r, W.RefNESResult) and r.worker_id == 11 for t, r in got)
+    if eval_prob:
+        want = worker.policy.rollout(None, batch, None)
+        assert all(r.eval_score == want and r.evolve_noise is None for _, r in got)
+        return
+    fit = eng.evaluate(tid, 0, 4, 0.05).numpy()
+    assert len(got) == 4
+    for k, (_, r) in enumerate(got):
+        assert np.array_equal(r.fitness, fit[k])
+        idx = O.noise_index(0, tid, k, table.size, dims.D)
+        assert r.evolve_noise.dtype == np.float32 and np.array_equal(r.evolve_noise, np.float32(0.05) * table[idx: idx + dims.D])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _wait(cond, timeout=120.0):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        v = cond()
+        if v:
+            return v
+        time.sleep(0.1)
+    raise TimeoutError
+
+
+def test_worker_pool_restarts_and_serves_the_engine_master(tmp_path):
+    from nicnes.worker import PID_KEY, STOP_KEY
+    dims, theta, fc, gts, df, n, table = tiny_workload()
+    batch = {'fc_feats': fc, 'gts': gts}
+    P = 4
+    local = M.EngineMaster(_spec(P), OracleEngine(dims, theta, fc, gts, df, n, table), log_dir=str(tmp_path / 'a'))
+    local.run([batch] * 2, max_iterations=2)
+
+    port = _free_port()
+    store = T.TCPStoreRedis('127.0.0.1', port, is_master=True)
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([REPO, os.path.join(REPO, 'nes-img-captioning_amd')]))
+    cmd = [sys.executable, '-m', 'nicnes.worker', '--store', 'tcp://127.0.0.1:%d' % port, '--num_workers', '2',
+           '--wire', 'engine', '--engine_factory', 'tests.worker_factory:oracle_engine', '--vocab_size', '63',
+           '--chunk', '2', '--check_interval', '0.2', '--noise_seed', '0']
+    pool = subprocess.Popen(cmd, env=env, cwd=REPO, start_new_session=True, stdout=subprocess.DEVNULL,
+                            stderr=subprocess.DEVNULL)
+    try:
+        master = M.EngineMaster(_spec(P), OracleEngine(dims, theta, fc, gts, df, n, table), log_dir=str(tmp_path / 'b'))
+        mc = T.MasterClient(store)
+        master.run_dispatched(mc, [batch], max_iterations=1, result_timeout=120)
+        pid0 = _wait(lambda: store.get(PID_KEY % 0))
+        os.kill(int(pid0), signal.SIGKILL)                     # a worker dies mid-run
+        _wait(lambda: (store.get(PID_KEY % 0) or pid0) != pid0)   # ... and comes back as a fresh process
+        master.run_dispatched(mc, [batch], max_iterations=1, result_timeout=120)
+        assert master.sched.iteration == 2
+        assert np.array_equal(master.e.theta()[0].numpy(), local.e.theta()[0].numpy())
+        store.set(STOP_KEY, b'1')
+        assert pool.wait(timeout=90) == 0
+    finally:
+        if pool.poll() is None:
+            os.killpg(pool.pid, signal.SIGKILL)
