@@ -73,6 +73,13 @@ int nicnes_get_adam_state(nicnes_handle* h, double* m_out, double* v_out, int64_
 int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t* ref_tokens, int32_t n_refs,
                      const int32_t* img_ref_start, void* stream);
 
+/* Several batches at once, for per-member batches (single_batch: false in the experiment JSON: each
+ * reference worker draws its own batch for every member, src/algorithm/nic_nes/nic_nes_worker.py:
+ * 121-128). fc [n_batches * B, F]; batch g holds images g * B .. g * B + B - 1, whose references are
+ * ranges of img_ref_start [n_batches * B + 1] as in nicnes_set_batch (= this call with n_batches 1). */
+int nicnes_set_batches(nicnes_handle* h, const float* fc, int32_t n_batches, int32_t B, const int32_t* ref_tokens,
+                       int32_t n_refs, const int32_t* img_ref_start, void* stream);
+
 /* Fixed document-frequency table (CiderD(df='coco-train-idxs'), src/captioning/policies.py:72):
  * sorted packed n-gram keys (n<<56 | t0<<42 | t1<<28 | t2<<14 | t3), df counts, and
  * ref_len = log(raw ref_len) as the scorer uses it. The engine keeps its own hashed copy, built
@@ -112,6 +119,13 @@ int nicnes_set_fitness_mode(nicnes_handle* h, int32_t mode);
  * (src/captioning/nets.py:191,208,241): logprob_out [count, 2, B, seq_length] fp32 or NULL. */
 int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
                        double* fitness_out, int32_t* seq_out, float* logprob_out, void* stream);
+
+/* nicnes_evaluate_lp where member member_begin + k decodes and is scored on batch
+ * member_batch_host[k] (a HOST array of count entries in [0, n_batches), copied before return) of
+ * the batches set by nicnes_set_batches. NULL = every member on batch 0 (only with one batch held). */
+int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
+                            const int32_t* member_batch_host, double* fitness_out, int32_t* seq_out, float* logprob_out,
+                            void* stream);
 
 /* Centred ranks + antithetic weights over the WHOLE population, replaces
  * NESMaster.compute_centered_ranks and the weights line of gradient_estimate

@@ -19,9 +19,9 @@ struct CiderTables {
     double* ref_norm;          // [n_refs, 4]
     // per-image n-gram tables (written by nicnes_img_ngram_kernel): the union of the image's
     // reference n-grams, hashed to a row of per-reference tf-idf weights
-    uint64_t* img_hkey;        // [B, IMG_CAP] (0 = empty)
-    int32_t* img_hrow;         // [B, IMG_CAP]
-    double* img_vr;            // [B, IMG_ROWS, IMG_MAXR]
+    uint64_t* img_hkey;        // [images, IMG_CAP] (0 = empty)
+    int32_t* img_hrow;         // [images, IMG_CAP]
+    double* img_vr;            // [images, IMG_ROWS, IMG_MAXR]
 };
 #define IMG_CAP 1024
 #define IMG_ROWS 512
@@ -36,9 +36,10 @@ extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int
                                                hipStream_t stream);
 // lp (nullable) [n_cand, B, T] per-step log-probs; crit = fitness criterion (nicnes_set_fitness_mode)
 // scores: scratch [n_cand, B] fp64 (per-row CIDEr-D, reduced by a second kernel)
+// member_batch (nullable) [n_cand / 2]: candidate c scores against images member_batch[c / 2] * B + b
 extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
-                                              const int32_t* img_ref_start, const float* lp, int crit,
-                                              double* scores, double* fitness_out, hipStream_t stream);
+                                              const int32_t* img_ref_start, const int32_t* member_batch, const float* lp,
+                                              int crit, double* scores, double* fitness_out, hipStream_t stream);
 extern "C" hipError_t nicnes_launch_cider(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
-                                          const int32_t* img_ref_start, const float* lp, int crit,
-                                          double* fitness_out, hipStream_t stream);
+                                          const int32_t* img_ref_start, const int32_t* member_batch, const float* lp,
+                                          int crit, double* fitness_out, hipStream_t stream);

@@ -194,11 +194,12 @@ __device__ void finish_fitness(const double* row_score, const int32_t* seq, cons
 
 // ---- candidates: one workgroup per candidate, one wave per image row ---------------------------
 __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, int B, int T, CiderTables tb,
-                                                           const int32_t* img_ref_start, const float* lp, int crit,
-                                                           double* fitness_out) {
+                                                           const int32_t* img_ref_start, const int32_t* member_batch,
+                                                           const float* lp, int crit, double* fitness_out) {
     __shared__ double row_score[1024];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int cand = blockIdx.x;
+    img_ref_start += member_batch ? member_batch[cand >> 1] * B : 0;     // this member's batch (single_batch: false)
     const double sigma2x2 = 2.0 * 6.0 * 6.0;
     for (int b = wave; b < B; b += 4) {
         const int32_t* row = seq + ((size_t)cand * B + b) * T;
@@ -261,11 +262,11 @@ extern "C" hipError_t nicnes_launch_cook_refs(const int32_t* ref_tokens, int n_r
 }
 
 extern "C" hipError_t nicnes_launch_cider(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
-                                          const int32_t* img_ref_start, const float* lp, int crit,
-                                          double* fitness_out, hipStream_t stream) {
+                                          const int32_t* img_ref_start, const int32_t* member_batch, const float* lp,
+                                          int crit, double* fitness_out, hipStream_t stream) {
     if (B > 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(nicnes_cider_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, *tb, img_ref_start, lp, crit,
-                       fitness_out);
+    hipLaunchKernelGGL(nicnes_cider_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, *tb, img_ref_start,
+                       member_batch, lp, crit, fitness_out);
     return hipGetLastError();
 }
 
@@ -316,9 +317,11 @@ __global__ __launch_bounds__(64) void nicnes_img_ngram_kernel(const int32_t* img
 // and nicnes_cider_finish_kernel reduces them in row order, as the single-workgroup form did.
 #define CIDER_IMG_ROWS 32
 __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* seq, int B, int T, CiderTables tb,
-                                                               const int32_t* img_ref_start, double* scores) {
+                                                               const int32_t* img_ref_start, const int32_t* member_batch,
+                                                               double* scores) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int cand = blockIdx.x;
+    const int img0 = member_batch ? member_batch[cand >> 1] * B : 0;      // this member's batch (single_batch: false)
     const int b_end = min(B, (int)(blockIdx.y + 1) * CIDER_IMG_ROWS);
     const double sigma2x2 = 2.0 * 6.0 * 6.0;
     for (int b = (int)blockIdx.y * CIDER_IMG_ROWS + wave; b < b_end; b += 4) {
@@ -331,15 +334,15 @@ __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* se
         if (g.first) {
             uint32_t slot = (uint32_t)df_hash(g.key) & (IMG_CAP - 1);
             for (int probe = 0; probe < IMG_CAP; ++probe) {
-                const uint64_t k = tb.img_hkey[(size_t)b * IMG_CAP + slot];
-                if (k == g.key) { trow = tb.img_hrow[(size_t)b * IMG_CAP + slot]; break; }
+                const uint64_t k = tb.img_hkey[(size_t)(img0 + b) * IMG_CAP + slot];
+                if (k == g.key) { trow = tb.img_hrow[(size_t)(img0 + b) * IMG_CAP + slot]; break; }
                 if (k == 0ull) break;
                 slot = (slot + 1) & (IMG_CAP - 1);
             }
         }
-        const double* vrow = tb.img_vr + ((size_t)b * IMG_ROWS + (trow >= 0 ? trow : 0)) * IMG_MAXR;
+        const double* vrow = tb.img_vr + ((size_t)(img0 + b) * IMG_ROWS + (trow >= 0 ? trow : 0)) * IMG_MAXR;
         double score = 0.0;
-        const int r0 = img_ref_start[b], r1 = img_ref_start[b + 1];
+        const int r0 = img_ref_start[img0 + b], r1 = img_ref_start[img0 + b + 1];
         for (int r = r0; r < r1; ++r) {
             const double vr = trow >= 0 ? vrow[r - r0] : 0.0;
             const double contrib = g.first ? (g.vec < vr ? g.vec : vr) * vr : 0.0;
@@ -376,11 +379,11 @@ extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int
 }
 
 extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
-                                              const int32_t* img_ref_start, const float* lp, int crit,
-                                              double* scores, double* fitness_out, hipStream_t stream) {
+                                              const int32_t* img_ref_start, const int32_t* member_batch, const float* lp,
+                                              int crit, double* scores, double* fitness_out, hipStream_t stream) {
     if (B > 1024 || n_cand < 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL(nicnes_cider_img_kernel, dim3(n_cand, (B + CIDER_IMG_ROWS - 1) / CIDER_IMG_ROWS), dim3(256), 0,
-                       stream, seq, B, T, *tb, img_ref_start, scores);
+                       stream, seq, B, T, *tb, img_ref_start, member_batch, scores);
     hipLaunchKernelGGL(nicnes_cider_finish_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, (const double*)scores,
                        lp, crit, fitness_out);
     return hipGetLastError();

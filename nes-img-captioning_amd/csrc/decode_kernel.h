@@ -9,7 +9,8 @@ struct DecodeParams {
     const float* theta;          // base theta, fp32 [D] (flat order: SURVEY.md Appendix A.1)
     const float* noise;          // shared Gaussian table, fp32 [noise_len]
     const uint64_t* noise_idx;   // per member slice start (multiple of 64)
-    const float* fc;             // unique-image fc features [B, F]
+    const float* fc;             // unique-image fc features [images, F]
+    const int32_t* member_batch; // nullable: member k of the launch decodes images member_batch[k] * B .. + B
     int32_t* seq;                // out: [members, 2, B, T] greedy tokens (masked after the first 0)
     float* lp;                   // out (nullable): [members, 2, B, T] log-prob of the greedy token (nets.py:208,241)
     float* scratch;              // nicnes_decode_scratch_floats(): lane-private c | h' | x0 | unfinished | h' (odd)

@@ -686,7 +686,8 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SCtx<G> c = make_sctx<G>(p);
     PROF_MARK(80);
-    const rsrc_t fc_r = make_rsrc(p.fc, 4u * (uint32_t)p.B * (uint32_t)p.F);
+    const float* fcm = p.fc + (p.member_batch ? (size_t)p.member_batch[c.member] * p.B * p.F : 0);
+    const rsrc_t fc_r = make_rsrc(fcm, 4u * (uint32_t)p.B * (uint32_t)p.F);
     const uint32_t lo = 4u * c.lane;
     const bool mm = G == 4 || c.hf == 0;
     StageRegs sr;

@@ -40,7 +40,11 @@ struct nicnes_handle {
     bool theta_set = false;
 
     const float* fc = nullptr;
-    int32_t B = 0;
+    int32_t B = 0;                    // rows (images) decoded per member
+    int32_t n_batches = 1;            // batches held (single_batch: false holds several)
+    int32_t n_img = 0;                // images held = n_batches * B
+    int32_t img_cap = 0;              // per-image CIDEr-D table capacity
+    int32_t* mbatch = nullptr;        // [max_members] member -> batch map of the current evaluate
     int32_t n_refs = 0;
     const int32_t* img_ref_start = nullptr;
     bool batch_set = false;
@@ -74,6 +78,9 @@ struct nicnes_handle {
     int32_t* alive = nullptr;         // per decode workgroup: rows left unfinished (fused [stride], split [2][stride])
     int32_t alive_stride = 0;         // max decode workgroups (members x 64-row slabs)
     float* part = nullptr;            // split decode: partial greedy states
+    uint64_t* rank_key = nullptr;     // rank sort scratch (grown to the largest population ranked)
+    uint32_t* rank_idx = nullptr;
+    size_t rank_cap = 0;
     int64_t part_cap = 0;             // in logit workgroups (members x slabs x S)
     int n_cu = 256;
     int dec_S = 0, dec_G = 0;         // nicnes_set_decode_split (0 = automatic)
@@ -192,27 +199,38 @@ int alloc_refs(nicnes_handle* h, int max_refs) {
 // Buffers sized by the batch: per-image n-gram tables, tokens / log-probs / row scores of a launch,
 // decode lane scratch, alive flags and partial states.
 int alloc_batch(nicnes_handle* h, int max_batch) {
-    void* old[] = {h->img_hkey, h->img_hrow, h->img_vr, h->seq, h->lp, h->row_scores, h->dscratch, h->alive, h->part};
+    void* old[] = {h->seq, h->lp, h->row_scores, h->dscratch, h->alive, h->part};
     for (void* q : old)
         if (q) (void)hipFree(q);
-    h->img_hkey = nullptr; h->img_hrow = nullptr; h->img_vr = nullptr; h->seq = nullptr; h->lp = nullptr;
-    h->row_scores = nullptr; h->dscratch = nullptr; h->alive = nullptr; h->part = nullptr;
+    h->seq = nullptr; h->lp = nullptr; h->row_scores = nullptr; h->dscratch = nullptr; h->alive = nullptr;
+    h->part = nullptr;
     const size_t MM = (size_t)h->cfg.max_members, MB = (size_t)max_batch, T = (size_t)h->cfg.seq_length;
     // lane scratch: 2G row waves per slab, the larger of the two slab layouts
     const int rw = std::max(8 * nslabs_of((int)MB, 4), 4 * nslabs_of((int)MB, 2));
     h->alive_stride = (int32_t)(MM * (size_t)nslabs_of((int)MB, 2));
     const int ns = std::max(nslabs_of((int)MB, 2), nslabs_of((int)MB, 4));
     h->part_cap = std::max(auto_part_cap((int)MM, (int)MB, h->n_cu), (int64_t)MM * ns * std::max(h->dec_S, 1));
-    int rc = dalloc(h, &h->img_hkey, MB * IMG_CAP);
-    if (!rc) rc = dalloc(h, &h->img_hrow, MB * IMG_CAP);
-    if (!rc) rc = dalloc(h, &h->img_vr, MB * IMG_ROWS * IMG_MAXR);
-    if (!rc) rc = dalloc(h, &h->seq, MM * 2 * MB * T);
+    int rc = dalloc(h, &h->seq, MM * 2 * MB * T);
     if (!rc) rc = dalloc(h, &h->lp, MM * 2 * MB * T);
     if (!rc) rc = dalloc(h, &h->row_scores, MM * 2 * MB);
     if (!rc) rc = dalloc(h, &h->dscratch, nicnes_decode_scratch_floats((int)MM, rw));
     if (!rc) rc = dalloc(h, &h->alive, 3 * (size_t)h->alive_stride);
     if (!rc) rc = dalloc(h, &h->part, (size_t)h->part_cap * PART_FLOATS);
     if (!rc) h->cfg.max_batch = max_batch;
+    return rc;
+}
+
+// Per-image CIDEr-D n-gram tables for every image held (all batches of a per-member-batch evaluate).
+int alloc_images(nicnes_handle* h, int n_img) {
+    void* old[] = {h->img_hkey, h->img_hrow, h->img_vr};
+    for (void* q : old)
+        if (q) (void)hipFree(q);
+    h->img_hkey = nullptr; h->img_hrow = nullptr; h->img_vr = nullptr;
+    const size_t N = (size_t)n_img;
+    int rc = dalloc(h, &h->img_hkey, N * IMG_CAP);
+    if (!rc) rc = dalloc(h, &h->img_hrow, N * IMG_CAP);
+    if (!rc) rc = dalloc(h, &h->img_vr, N * IMG_ROWS * IMG_MAXR);
+    if (!rc) h->img_cap = n_img;
     return rc;
 }
 
@@ -281,8 +299,15 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
     if (!rc) rc = dalloc(h, &h->stats, 4);
     if (!rc) rc = dalloc(h, &h->partials, 2 * (size_t)nicnes_adam_blocks(h->D));
     if (!rc) rc = dalloc(h, &h->norms, 2);
+    if (!rc) {
+        h->rank_cap = nicnes_rank_scratch_pairs(2 * cfg->max_members);
+        rc = dalloc(h, &h->rank_key, h->rank_cap);
+        if (!rc) rc = dalloc(h, &h->rank_idx, h->rank_cap);
+    }
     if (!rc) rc = alloc_refs(h, cfg->max_refs);
     if (!rc) rc = alloc_batch(h, cfg->max_batch);
+    if (!rc) rc = alloc_images(h, cfg->max_batch);
+    if (!rc) rc = dalloc(h, &h->mbatch, (size_t)cfg->max_members);
     if (rc) {
         nicnes_destroy(h);
         return rc;
@@ -304,7 +329,8 @@ int nicnes_destroy(nicnes_handle* h) {
     if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
                     h->ref_norm, h->nidx, h->seq, h->lp, h->row_scores, h->dscratch, h->stats, h->partials, h->norms,
-                    h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive, h->part};
+                    h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive, h->part,
+                    h->rank_key, h->rank_idx, h->mbatch};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : h->ev)
@@ -415,22 +441,25 @@ int nicnes_set_df_table(nicnes_handle* h, const uint64_t* keys, const double* df
     return NICNES_OK;
 }
 
-int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t* ref_tokens, int32_t n_refs,
-                     const int32_t* img_ref_start, void* stream) {
+int nicnes_set_batches(nicnes_handle* h, const float* fc, int32_t n_batches, int32_t B, const int32_t* ref_tokens,
+                       int32_t n_refs, const int32_t* img_ref_start, void* stream) {
     if (!h || !fc || !ref_tokens || !img_ref_start) return NICNES_ERR_INVALID;
     if (B < 1 || B > 1024) return fail(h, NICNES_ERR_INVALID, "B out of [1, 1024]");
-    if (n_refs < B) return fail(h, NICNES_ERR_INVALID, "n_refs < B");
+    if (n_batches < 1 || (int64_t)n_batches * B > (1 << 20)) return fail(h, NICNES_ERR_INVALID, "n_batches out of range");
+    const int n_img = n_batches * B;
+    if (n_refs < n_img) return fail(h, NICNES_ERR_INVALID, "n_refs < images");
     if (!h->df_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_df_table first");
     if (((uintptr_t)fc & 15u) != 0) return fail(h, NICNES_ERR_INVALID, "fc must be 16-byte aligned");
     HIPC(h, hipSetDevice(h->device));
-    // a batch-size curriculum (bs_multiplier, tools/iteration.py:149-153) can outgrow the sizes the
-    // handle was created with: re-create the batch buffers (outside every evaluate, so no launch
-    // in flight uses them once the device is idle)
-    if (B > h->cfg.max_batch || n_refs > h->cfg.max_refs) {
+    // a batch-size curriculum (bs_multiplier, tools/iteration.py:149-153) or more batches can outgrow
+    // the sizes the handle was created with: re-create those buffers (outside every evaluate, so no
+    // launch in flight uses them once the device is idle)
+    if (B > h->cfg.max_batch || n_refs > h->cfg.max_refs || n_img > h->img_cap) {
         HIPC(h, hipDeviceSynchronize());
         int rc = NICNES_OK;
         if (n_refs > h->cfg.max_refs) rc = alloc_refs(h, std::max(n_refs, 2 * h->cfg.max_refs));
         if (!rc && B > h->cfg.max_batch) rc = alloc_batch(h, B);
+        if (!rc && n_img > h->img_cap) rc = alloc_images(h, n_img);
         if (rc) {
             h->batch_set = false;
             return rc;
@@ -438,13 +467,13 @@ int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t
     }
     // reference ranges: CiderD asserts every image has references (len(ref) > 0, upstream
     // cider_scorer); ranges must tile [0, n_refs)
-    std::vector<int32_t> st((size_t)B + 1);
+    std::vector<int32_t> st((size_t)n_img + 1);
     HIPC(h, hipMemcpyAsync(st.data(), img_ref_start, st.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
                            (hipStream_t)stream));
     HIPC(h, hipStreamSynchronize((hipStream_t)stream));
     int maxr = 0;
-    bool ok = st[0] == 0 && st[B] == n_refs;
-    for (int b = 0; b < B && ok; ++b) {
+    bool ok = st[0] == 0 && st[n_img] == n_refs;
+    for (int b = 0; b < n_img && ok; ++b) {
         ok = st[b + 1] > st[b];
         maxr = std::max(maxr, st[b + 1] - st[b]);
     }
@@ -454,6 +483,8 @@ int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t
     }
     h->fc = fc;
     h->B = B;
+    h->n_batches = n_batches;
+    h->n_img = n_img;
     h->n_refs = n_refs;
     h->img_ref_start = img_ref_start;
     CiderTables tb = tables_of(h);
@@ -462,11 +493,16 @@ int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t
     // per-reference scan kernel scores the candidates)
     h->img_tables = maxr <= IMG_MAXR;
     if (h->img_tables) {
-        HIPC(h, hipMemsetAsync(h->img_vr, 0, (size_t)B * IMG_ROWS * IMG_MAXR * sizeof(double), (hipStream_t)stream));
-        HIPC(h, nicnes_launch_img_ngrams(img_ref_start, B, &tb, (hipStream_t)stream));
+        HIPC(h, hipMemsetAsync(h->img_vr, 0, (size_t)n_img * IMG_ROWS * IMG_MAXR * sizeof(double), (hipStream_t)stream));
+        HIPC(h, nicnes_launch_img_ngrams(img_ref_start, n_img, &tb, (hipStream_t)stream));
     }
     h->batch_set = true;
     return NICNES_OK;
+}
+
+int nicnes_set_batch(nicnes_handle* h, const float* fc, int32_t B, const int32_t* ref_tokens, int32_t n_refs,
+                     const int32_t* img_ref_start, void* stream) {
+    return nicnes_set_batches(h, fc, 1, B, ref_tokens, n_refs, img_ref_start, stream);
 }
 
 int nicnes_noise_indices(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, uint64_t* out,
@@ -506,6 +542,13 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
 
 int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
                        double* fitness_out, int32_t* seq_out, float* logprob_out, void* stream) {
+    return nicnes_evaluate_batches(h, iteration, member_begin, count, sigma, nullptr, fitness_out, seq_out, logprob_out,
+                                   stream);
+}
+
+int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
+                            const int32_t* member_batch_host, double* fitness_out, int32_t* seq_out, float* logprob_out,
+                            void* stream) {
     if (!h || !fitness_out || member_begin < 0) return NICNES_ERR_INVALID;
     if (count < 1 || count > h->cfg.max_members) return fail(h, NICNES_ERR_INVALID, "count out of [1, max_members]");
     if (!h->noise) return fail(h, NICNES_ERR_INVALID, "nicnes_set_noise_table first");
@@ -513,6 +556,17 @@ int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begi
     if (!h->batch_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_batch first");
     hipStream_t s = (hipStream_t)stream;
     HIPC(h, hipSetDevice(h->device));
+    const int32_t* mb = nullptr;
+    if (member_batch_host) {
+        for (int k = 0; k < count; ++k)
+            if (member_batch_host[k] < 0 || member_batch_host[k] >= h->n_batches)
+                return fail(h, NICNES_ERR_INVALID, "member_batch entry outside [0, n_batches)");
+        HIPC(h, hipMemcpyAsync(h->mbatch, member_batch_host, (size_t)count * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        HIPC(h, hipStreamSynchronize(s));        // the caller's host array may go away on return
+        mb = h->mbatch;
+    } else if (h->n_batches != 1) {
+        return fail(h, NICNES_ERR_INVALID, "several batches are held: pass member_batch (nicnes_evaluate_batches)");
+    }
     HIPC(h, nicnes_launch_noise_index(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, h->cfg.noise_len,
                                       (uint64_t)h->D, h->nidx, s));
     DecodeParams p;
@@ -520,6 +574,7 @@ int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begi
     p.noise = h->noise;
     p.noise_idx = h->nidx;
     p.fc = h->fc;
+    p.member_batch = mb;
     p.seq = seq_out ? seq_out : h->seq;
     p.lp = logprob_out ? logprob_out : (h->fitness_mode ? h->lp : nullptr);
     p.scratch = h->dscratch;
@@ -560,20 +615,33 @@ int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begi
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     CiderTables tb = tables_of(h);
     if (h->img_tables)
-        HIPC(h, nicnes_launch_cider_img(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, p.lp,
+        HIPC(h, nicnes_launch_cider_img(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
                                          h->fitness_mode, h->row_scores, fitness_out, s));
     else
-        HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, p.lp,
-                                         h->fitness_mode, fitness_out, s));
+        HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
+                                    h->fitness_mode, fitness_out, s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[2], s));
     return NICNES_OK;
 }
 
 int nicnes_rank_weights(nicnes_handle* h, const double* fitness, int32_t P, double* cr_out, float* w_out, void* stream) {
     if (!h || !fitness || !w_out || P < 1) return NICNES_ERR_INVALID;
-    if (P > 5120) return fail(h, NICNES_ERR_UNSUPPORTED, "P > 5120");
+    if (P > (1 << 29)) return fail(h, NICNES_ERR_UNSUPPORTED, "P > 2^29");
     HIPC(h, hipSetDevice(h->device));
-    HIPC(h, nicnes_launch_rank(fitness, 2 * P, cr_out, w_out, (hipStream_t)stream));
+    const size_t need = nicnes_rank_scratch_pairs(2 * P);
+    if (need > h->rank_cap) {       // the first call at a larger population grows the sort scratch
+        HIPC(h, hipStreamSynchronize((hipStream_t)stream));
+        if (h->rank_key) (void)hipFree(h->rank_key);
+        if (h->rank_idx) (void)hipFree(h->rank_idx);
+        h->rank_key = nullptr;
+        h->rank_idx = nullptr;
+        h->rank_cap = 0;
+        int rc = dalloc(h, &h->rank_key, need);
+        if (!rc) rc = dalloc(h, &h->rank_idx, need);
+        if (rc) return rc;
+        h->rank_cap = need;
+    }
+    HIPC(h, nicnes_launch_rank(fitness, 2 * P, h->rank_key, h->rank_idx, cr_out, w_out, (hipStream_t)stream));
     return NICNES_OK;
 }
 

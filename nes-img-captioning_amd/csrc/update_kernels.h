@@ -28,7 +28,9 @@ extern "C" hipError_t nicnes_launch_noise_index(uint64_t seed, uint64_t iteratio
                                                 uint64_t table_len, uint64_t dim, uint64_t* out, hipStream_t s);
 extern "C" hipError_t nicnes_launch_noise_vectors(const float* noise, const uint64_t* idx, int count, int64_t dim,
                                                   float sigma, float* out, hipStream_t s);
-extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, double* cr_out, float* w_out, hipStream_t s);
+extern "C" size_t nicnes_rank_scratch_pairs(int n);
+extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, uint64_t* skey, uint32_t* sidx, double* cr_out,
+                                         float* w_out, hipStream_t s);
 extern "C" hipError_t nicnes_launch_grad(const float* noise, const uint64_t* idx, const float* w, int count, float sigma,
                                          int64_t dim, float* gsum, hipStream_t s);
 extern "C" int nicnes_adam_blocks(int64_t dim);

@@ -23,28 +23,87 @@ __global__ void nicnes_noise_index_kernel(uint64_t seed, uint64_t iteration, uin
     if (i < count) out[i] = nn_noise_index(seed, iteration, member0 + (uint64_t)i, table_len, dim);
 }
 
-// rank_i = #{j : x_j < x_i} + #{j < i : x_j == x_i}  over the ravelled (P, 2) fitness
-__global__ __launch_bounds__(1024) void nicnes_rank_kernel(const double* fit, int n, double* cr_out, float* w_out) {
-    extern __shared__ double xs[];
-    for (int i = threadIdx.x; i < n; i += blockDim.x) xs[i] = fit[i];
-    __syncthreads();
-    double* crs = xs + n;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const double xi = xs[i];
-        int rank = 0;
-        for (int j = 0; j < n; ++j) {
-            const double xj = xs[j];
-            rank += (xj < xi) || (xj == xi && j < i);
-        }
-        double y = (double)rank;
-        y /= (double)(n - 1);                  // y /= (x.size - 1)
-        y -= 0.5;                              // y -= .5
-        crs[i] = y;
-        if (cr_out) cr_out[i] = y;
+// ---- centred ranks: rank_i = #{j : (x_j, j) < (x_i, i)} over the ravelled (P, 2) fitness -----
+// The reference sorts with numpy's default argsort (compute_ranks, nic_nes_master.py:196-205); the
+// engine's order is the stable one, (value, index), identical whenever values are distinct. Values
+// map to an order-preserving uint64 (-0.0 as +0.0, every NaN as one NaN sorting last, as numpy's
+// argsort places NaN). Pass 1: each workgroup bitonic-sorts a chunk of RANK_CHUNK (key, index)
+// pairs in LDS. Pass 2: a pair's rank is the sum over chunks of its lower bound in that chunk
+// (binary search); keys are unique with the index, so this is the stable rank. Any population size.
+#define RANK_CHUNK 2048
+
+__device__ __forceinline__ uint64_t rank_key(double x) {
+    if (x != x) x = __builtin_nan("");                      // one canonical (positive) NaN: last
+    if (x == 0.0) x = 0.0;                                  // -0.0 == 0.0
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ bool pair_less(uint64_t ka, uint32_t ia, uint64_t kb, uint32_t ib) {
+    return ka < kb || (ka == kb && ia < ib);
+}
+
+__global__ __launch_bounds__(1024) void nicnes_rank_sort_kernel(const double* fit, int n, uint64_t* skey, uint32_t* sidx) {
+    __shared__ uint64_t k[RANK_CHUNK];
+    __shared__ uint32_t ix[RANK_CHUNK];
+    const int base = blockIdx.x * RANK_CHUNK;
+    for (int e = threadIdx.x; e < RANK_CHUNK; e += blockDim.x) {
+        const int g = base + e;
+        k[e] = g < n ? rank_key(fit[g]) : ~0ull;            // padding sorts after every real pair
+        ix[e] = g < n ? (uint32_t)g : 0xffffffffu;
     }
     __syncthreads();
-    for (int p = threadIdx.x; p < n / 2; p += blockDim.x)
-        w_out[p] = (float)(crs[2 * p] - crs[2 * p + 1]);     // cr[:, 0] - cr[:, 1], then fp32 dot
+    for (int size = 2; size <= RANK_CHUNK; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            const int t = threadIdx.x;                      // one compare-exchange per thread
+            const int a = 2 * t - (t & (stride - 1));
+            const int b = a + stride;
+            const bool up = (a & size) == 0;
+            const uint64_t ka = k[a], kb = k[b];
+            const uint32_t ia = ix[a], ib = ix[b];
+            if (pair_less(kb, ib, ka, ia) == up) {
+                k[a] = kb; k[b] = ka;
+                ix[a] = ib; ix[b] = ia;
+            }
+            __syncthreads();
+        }
+    }
+    for (int e = threadIdx.x; e < RANK_CHUNK; e += blockDim.x) {
+        skey[base + e] = k[e];
+        sidx[base + e] = ix[e];
+    }
+}
+
+__device__ __forceinline__ int chunk_lower_bound(const uint64_t* key, const uint32_t* idx, uint64_t kq, uint32_t iq) {
+    int lo = 0, hi = RANK_CHUNK;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (pair_less(key[mid], idx[mid], kq, iq)) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void nicnes_rank_kernel(const double* fit, int n, const uint64_t* skey,
+                                                          const uint32_t* sidx, double* cr_out, float* w_out) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (2 * p >= n) return;
+    const int nchunks = (n + RANK_CHUNK - 1) / RANK_CHUNK;
+    double cr[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int e = 2 * p + s;
+        const uint64_t kq = rank_key(fit[e]);
+        int rank = 0;
+        for (int c = 0; c < nchunks; ++c)
+            rank += chunk_lower_bound(skey + (size_t)c * RANK_CHUNK, sidx + (size_t)c * RANK_CHUNK, kq, (uint32_t)e);
+        double y = (double)rank;
+        y /= (double)(n - 1);                  // y /= (x.size - 1)   (compute_centered_ranks)
+        y -= 0.5;                              // y -= .5
+        cr[s] = y;
+        if (cr_out) cr_out[e] = y;
+    }
+    w_out[p] = (float)(cr[0] - cr[1]);         // cr[:, 0] - cr[:, 1], then fp32 (gradient_estimate)
 }
 
 // gsum[j] = fp32( sum_i w_i * fp32(sigma * z[idx_i + j]) ), fp64 accumulation in member order
@@ -173,14 +232,13 @@ extern "C" hipError_t nicnes_launch_noise_index(uint64_t seed, uint64_t iteratio
     return hipGetLastError();
 }
 
-extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, double* cr_out, float* w_out, hipStream_t s) {
-    const size_t lds = (size_t)2 * n * sizeof(double);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
-    if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)nicnes_rank_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(nicnes_rank_kernel, dim3(1), dim3(1024), lds, s, fit, n, cr_out, w_out);
+extern "C" size_t nicnes_rank_scratch_pairs(int n) { return (size_t)((n + RANK_CHUNK - 1) / RANK_CHUNK) * RANK_CHUNK; }
+
+extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, uint64_t* skey, uint32_t* sidx, double* cr_out,
+                                         float* w_out, hipStream_t s) {
+    const int nchunks = (n + RANK_CHUNK - 1) / RANK_CHUNK;
+    hipLaunchKernelGGL(nicnes_rank_sort_kernel, dim3(nchunks), dim3(RANK_CHUNK / 2), 0, s, fit, n, skey, sidx);
+    hipLaunchKernelGGL(nicnes_rank_kernel, dim3((n / 2 + 255) / 256), dim3(256), 0, s, fit, n, skey, sidx, cr_out, w_out);
     return hipGetLastError();
 }
 

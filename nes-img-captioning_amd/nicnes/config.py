@@ -96,6 +96,22 @@ class ExperimentSpec:
         return self.policy_options.fitness or 'greedy'
 
     @property
+    def single_batch(self):
+        """config.single_batch: True = every member on the task's one batch; falsy (the reference's
+        default, and mscoco_nes.json's false) = every member on its own batch, as each reference
+        worker draws one per member (nic_nes_worker.py:121-128)."""
+        return bool(self.config.single_batch)
+
+    @property
+    def batches_per_iteration(self):
+        """Distinct batches per iteration: 1 with single_batch, else one per member, capped by the
+        engine-only key 'batches_per_iteration' (members then share batches round-robin)."""
+        if self.single_batch:
+            return 1
+        cap = int(self.exp.get('batches_per_iteration') or self.nb_offspring)
+        return max(1, min(self.nb_offspring, cap))
+
+    @property
     def sigma(self):
         return float(self.config.noise_stdev)
 

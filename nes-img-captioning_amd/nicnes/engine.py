@@ -132,22 +132,34 @@ class Engine:
     def set_batch(self, fc, gts):
         """fc [B, F] fp32 of unique images; gts: per image an int array [n_i, seq_length] of
         zero-padded label rows (data['gts'], /root/reference/src/captioning/dataloader.py:162)."""
-        fc_t = self._dev(fc, torch.float32)
-        B = fc_t.shape[0]
-        if len(gts) != B:
-            raise ValueError('gts has %d images, fc has %d rows' % (len(gts), B))
-        rows, start = [], [0]
-        for g in gts:
-            g = np.asarray(g, np.int32).reshape(-1, self.cfg.seq_length)
-            rows.append(g)
-            start.append(start[-1] + g.shape[0])
+        self.set_batches([(fc, gts)])
+
+    def set_batches(self, batches):
+        """Several batches of equal size B at once, [(fc [B, F], gts), ...], for per-member batches
+        (single_batch: false, /root/reference/src/algorithm/nic_nes/nic_nes_worker.py:121-128): an
+        evaluate's member_batch then names each member's batch."""
+        fcs, rows, start = [], [], [0]
+        for fc, gts in batches:
+            fc_np = fc.detach().cpu().numpy() if isinstance(fc, torch.Tensor) else np.asarray(fc, np.float32)
+            if len(gts) != fc_np.shape[0]:
+                raise ValueError('gts has %d images, fc has %d rows' % (len(gts), fc_np.shape[0]))
+            fcs.append(np.asarray(fc_np, np.float32))
+            for g in gts:
+                g = np.asarray(g, np.int32).reshape(-1, self.cfg.seq_length)
+                rows.append(g)
+                start.append(start[-1] + g.shape[0])
+        B = fcs[0].shape[0]
+        if any(f.shape[0] != B for f in fcs):
+            raise ValueError('batches must have the same number of images')
+        fc_t = self._dev(np.concatenate(fcs, 0), torch.float32)
         refs = self._dev(np.concatenate(rows, 0), torch.int32)
         starts = self._dev(np.array(start, np.int32), torch.int32)
         self._keep['fc'], self._keep['refs'], self._keep['ref_start'] = fc_t, refs, starts
         with torch.cuda.device(self.device):
-            check(self.L.nicnes_set_batch(self.h, _ptr(fc_t), B, _ptr(refs), int(refs.shape[0]), _ptr(starts),
-                                          self._stream()), self.h, 'set_batch')
+            check(self.L.nicnes_set_batches(self.h, _ptr(fc_t), len(fcs), B, _ptr(refs), int(refs.shape[0]),
+                                            _ptr(starts), self._stream()), self.h, 'set_batches')
         self.B = B
+        self.n_batches = len(fcs)
 
     # ---------------------------------------------------------------- the hot path -------
     def noise_indices(self, iteration, member_begin, count):
@@ -178,19 +190,27 @@ class Engine:
         check(self.L.nicnes_set_fitness_mode(self.h, code), self.h, 'set_fitness_mode(%r)' % (fitness,))
         self.fitness_mode = code
 
-    def evaluate(self, iteration, member_begin, count, sigma, fitness_out=None, return_seq=False, return_lp=False):
+    def evaluate(self, iteration, member_begin, count, sigma, fitness_out=None, return_seq=False, return_lp=False,
+                 member_batch=None):
         """Fitness (f+, f-) of members [member_begin, +count): tensor [count, 2] fp64 on the GPU.
         return_seq / return_lp add the greedy tokens [count, 2, B, T] int32 and their per-step
-        log-probs (FCModel._sample's seq_logprobs) [count, 2, B, T] fp32."""
+        log-probs (FCModel._sample's seq_logprobs) [count, 2, B, T] fp32. member_batch: per member the
+        index of its batch among set_batches' (None: the one batch held)."""
         fit = fitness_out if fitness_out is not None else torch.empty((count, 2), dtype=torch.float64,
                                                                       device=self.device)
         shape = (count, 2, self.B, self.cfg.seq_length)
         seq = torch.empty(shape, dtype=torch.int32, device=self.device) if return_seq else None
         lp = torch.empty(shape, dtype=torch.float32, device=self.device) if return_lp else None
+        mb = None
+        if member_batch is not None:
+            mb_np = np.ascontiguousarray(np.asarray(member_batch, np.int32))
+            if mb_np.shape != (count,):
+                raise ValueError('member_batch needs one entry per member')
+            mb = mb_np.ctypes.data_as(ctypes.c_void_p)
         with torch.cuda.device(self.device):
-            check(self.L.nicnes_evaluate_lp(self.h, ctypes.c_uint64(iteration), member_begin, count,
-                                            ctypes.c_float(sigma), _ptr(fit), _ptr(seq), _ptr(lp), self._stream()),
-                  self.h, 'evaluate')
+            check(self.L.nicnes_evaluate_batches(self.h, ctypes.c_uint64(iteration), member_begin, count,
+                                                 ctypes.c_float(sigma), mb, _ptr(fit), _ptr(seq), _ptr(lp),
+                                                 self._stream()), self.h, 'evaluate')
         out = (fit,) + ((seq,) if return_seq else ()) + ((lp,) if return_lp else ())
         return out if len(out) > 1 else fit
 

@@ -88,13 +88,25 @@ class EngineMaster:
         self.opt = make_optimizer(engine, spec)
         self.stats = []
         self._batch_key = None
+        self._n_batches = 1
 
     # ------------------------------------------------------------------------ helpers ----------
     def _set_batch(self, batch):
-        # the batch object itself is kept: an id() of a freed batch can be reused by the next one
+        """One batch (dict, or (fc, gts)) shared by every member, or a list of G batches (single_batch:
+        false: member i uses batch i mod G). The batch object itself is kept: an id() of a freed batch
+        can be reused by the next one."""
         if batch is not self._batch_key:
-            fc, gts = unique_batch(batch) if isinstance(batch, dict) else batch
-            self.e.set_batch(fc, gts)
+            if isinstance(batch, list):
+                ub = [unique_batch(b) if isinstance(b, dict) else b for b in batch]
+                if len(ub) == 1:
+                    self.e.set_batch(*ub[0])
+                else:
+                    self.e.set_batches(ub)
+                self._n_batches = len(ub)
+            else:
+                fc, gts = unique_batch(batch) if isinstance(batch, dict) else batch
+                self.e.set_batch(fc, gts)
+                self._n_batches = 1
             self._batch_key = batch
 
     def _update(self, gsum, P):
@@ -125,8 +137,12 @@ class EngineMaster:
         is evaluated (the reference restarts its loader with the new size, tools/iteration.py:150-154);
         any other iterable is consumed as given, one pass per epoch."""
         if hasattr(batches, 'get_batch'):
+            G = self.spec.batches_per_iteration
             while True:
-                yield batches.get_batch('train', batch_size=self.sched.batch_size)
+                if G == 1:
+                    yield batches.get_batch('train', batch_size=self.sched.batch_size)
+                else:          # single_batch: false -- one batch per member (nic_nes_worker.py:121-128)
+                    yield [batches.get_batch('train', batch_size=self.sched.batch_size) for _ in range(G)]
         for b in batches:
             yield b
 
@@ -150,7 +166,7 @@ class EngineMaster:
                 if runner is None or runner.sigma != self.sched.noise_stdev:
                     runner = PopulationRunner(self.e, P, self.sched.noise_stdev, rank=self.rank,
                                               world_size=self.world, group=self.group, comm=self.comm)
-                runner.evaluate(self.sched.iteration)
+                runner.evaluate(self.sched.iteration, n_batches=self._n_batches)
                 fit = runner.exchange_fitness()
                 _, w = self.e.rank_weights(fit)
                 self.e.grad_partial(self.sched.iteration, runner.m0, runner.local,

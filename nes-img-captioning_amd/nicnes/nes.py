@@ -77,6 +77,14 @@ def unique_batch(data, seq_per_img=5):
     return np.ascontiguousarray(fc), gts
 
 
+def member_batches(batch_data, member_begin, count):
+    """Per-member batch indices when batch_data is a list of G batches (member i uses batch i mod G),
+    None for one shared batch."""
+    if isinstance(batch_data, (list, tuple)) and len(batch_data) > 1:
+        return [(member_begin + k) % len(batch_data) for k in range(count)]
+    return None
+
+
 # ---------------------------------------------------------------- policy (Policy API) ------------
 class EnginePolicy:
     """Policy / CaptPolicy for the engine: theta lives on the GPU (fp64 master + fp32 copy)."""
@@ -124,19 +132,30 @@ class EnginePolicy:
         return int(self.e.noise_indices(iteration, member, 1).cpu()[0])
 
     def _ensure_batch(self, data, seq_per_img=5):
-        # the batch object itself is kept: an id() of a freed batch can be reused by the next one
+        """Load the batch (a reference batch dict) or the batches (a list of them, single_batch: false)
+        unless this very object is already loaded. The object itself is kept: an id() of a freed batch
+        can be reused by the next one."""
         if data is not self._batch_key:
-            fc, gts = unique_batch(data, seq_per_img)
-            self.e.set_batch(fc, gts)
+            if isinstance(data, (list, tuple)):
+                ub = [unique_batch(d, seq_per_img) for d in data]
+                if len(ub) == 1:
+                    self.e.set_batch(*ub[0])
+                else:
+                    self.e.set_batches(ub)
+                rows = ub[0][0].shape[0]
+            else:
+                fc, gts = unique_batch(data, seq_per_img)
+                self.e.set_batch(fc, gts)
+                rows = fc.shape[0]
             self._batch_key = data
-            self._batch_rows = fc.shape[0]
+            self._batch_rows = rows
         return self._batch_rows
 
     def rollout(self, placeholder, data, config):
         """CaptPolicy.rollout (policies.py:86-128) of the current theta: float(100 * mean CIDEr-D) for
         'greedy', the criterion value for the greedy_* fitness modes."""
         self._ensure_batch(data)
-        fit = self.e.evaluate(0, 0, 1, 0.0)
+        fit = self.e.evaluate(0, 0, 1, 0.0, member_batch=member_batches(data, 0, 1))
         return float(fit[0, 0].item())
 
 
@@ -166,7 +185,8 @@ class EngineWorker:
         """-> list of NESResult(fitness=[f+, f-] fp64, noise_idx, member)."""
         self._prepare(task_id, task_data)
         it = int(task_data.iteration if task_data.iteration is not None else task_id)
-        fit = self.e.evaluate(it, member_begin, count, float(task_data.noise_stdev)).cpu().numpy()
+        fit = self.e.evaluate(it, member_begin, count, float(task_data.noise_stdev),
+                              member_batch=member_batches(task_data.batch_data, member_begin, count)).cpu().numpy()
         idx = self.e.noise_indices(it, member_begin, count).cpu().numpy()
         return [NESResult(worker_id=self.worker_id, fitness=fit[k].copy(), noise_idx=int(idx[k]),
                           member=member_begin + k) for k in range(count)]

@@ -35,9 +35,14 @@ class PopulationRunner:
         self.fit_all = torch.empty((self.P, 2), dtype=torch.float64, device=dev) if world_size > 1 else self.fit_local
         self.gsum = torch.empty(engine.D, dtype=torch.float32, device=dev)
 
-    def evaluate(self, iteration):
-        """this rank's members -> fitness [local, 2] (f+, f-)"""
-        self.e.evaluate(iteration, self.m0, self.local, self.sigma, fitness_out=self.fit_local)
+    def evaluate(self, iteration, n_batches=1):
+        """this rank's members -> fitness [local, 2] (f+, f-). With n_batches > 1 (the engine holds
+        that many batches, single_batch: false) member i is scored on batch i mod n_batches."""
+        mb = None if n_batches <= 1 else [(self.m0 + k) % n_batches for k in range(self.local)]
+        if mb is None:
+            self.e.evaluate(iteration, self.m0, self.local, self.sigma, fitness_out=self.fit_local)
+        else:
+            self.e.evaluate(iteration, self.m0, self.local, self.sigma, fitness_out=self.fit_local, member_batch=mb)
         return self.fit_local
 
     def exchange_fitness(self):

@@ -42,6 +42,10 @@ class OracleEngine:
 
     def set_batch(self, fc, gts):
         self.fc, self.gts = np.asarray(fc, np.float32), gts
+        self.batches = None
+
+    def set_batches(self, batches):
+        self.batches = [(np.asarray(f, np.float32), g) for f, g in batches]
 
     def noise_indices(self, iteration, member_begin, count):
         return torch.tensor([self._idx(iteration, member_begin + k) for k in range(count)], dtype=torch.int64)
@@ -71,13 +75,14 @@ class OracleEngine:
     def _idx(self, iteration, m):
         return O.noise_index(self.seed, iteration, m, self.table.size, self.D)
 
-    def evaluate(self, iteration, member_begin, count, sigma, fitness_out=None):
+    def evaluate(self, iteration, member_begin, count, sigma, fitness_out=None, member_batch=None):
         out = fitness_out if fitness_out is not None else torch.empty((count, 2), dtype=torch.float64)
         for k in range(count):
             idx = self._idx(iteration, member_begin + k)
+            fc, gts = (self.fc, self.gts) if member_batch is None else self.batches[member_batch[k]]
             for s, sign in enumerate((+1, -1)):
-                seq, lp, _ = O.decode(self.dims, O.perturb(self.theta32, self.table, idx, sigma, sign), self.fc)
-                f, scores = CR.rollout_fitness(self.scorer, seq, self.gts)
+                seq, lp, _ = O.decode(self.dims, O.perturb(self.theta32, self.table, idx, sigma, sign), fc)
+                f, scores = CR.rollout_fitness(self.scorer, seq, gts)
                 out[k, s] = CR.criterion_fitness(self.fitness_mode, lp, seq, scores) if self.fitness_mode else f
         return out
 

@@ -285,7 +285,7 @@ def test_curriculum_draws_batches_at_the_scheduled_size():
     """bs_multiplier (tools/iteration.py:149-153): with a loader the master asks for batches of the
     scheduled size, so a batch-size curriculum changes what is evaluated; stepsize_divisor applies."""
     dims, theta, fc, gts, df, n, table = tiny_workload(B=8)
-    spec = _sched_spec(2, 2, schedule_start=1, schedule_limit=2, bs_multiplier=2, stepsize_divisor=4)
+    spec = _sched_spec(2, 2, schedule_start=1, schedule_limit=2, bs_multiplier=2, stepsize_divisor=4, single_batch=True)
     eng = OracleEngine(dims, theta, fc, gts, df, n, table)
     seen = []
     orig = eng.set_batch
@@ -355,3 +355,34 @@ def test_set_batch_not_skipped_when_an_id_is_reused(workload):
     for k in range(3):
         m._set_batch({'fc_feats': fc[:k + 1], 'gts': gts[:k + 1]})       # each dict freed right after
     assert loads == [1, 2, 3]
+
+
+def test_per_member_batches_single_batch_false():
+    """single_batch false (mscoco_nes.json; nic_nes_worker.py:121-128 draws a batch per member): the
+    master asks the loader for one batch per member (capped by batches_per_iteration) and member i
+    is scored on batch i mod G, locally and through a dispatched worker alike."""
+    dims, theta, fc, gts, df, n, table = tiny_workload(B=12)
+    P = 4
+    exp = _sched_spec(P, 3).exp
+    exp['config']['single_batch'] = False
+    exp['batches_per_iteration'] = 3
+    spec = C.ExperimentSpec(exp, vocab_size=63)
+    assert not spec.single_batch and spec.batches_per_iteration == 3
+    eng = OracleEngine(dims, theta, fc, gts, df, n, table)
+    loader = _Loader(fc, gts)
+    m = M.EngineMaster(spec, eng)
+    m.run(loader, max_iterations=1)
+    assert loader.sizes == [3, 3, 3]
+    # the fitness of member i is the one of batch i mod 3
+    ref = OracleEngine(dims, theta, fc, gts, df, n, table)
+    batches = [(fc[3 * g: 3 * g + 3], gts[3 * g: 3 * g + 3]) for g in range(3)]
+    fit = np.zeros((P, 2))
+    for i in range(P):
+        ref.set_batch(*batches[i % 3])
+        fit[i] = ref.evaluate(1, i, 1, 0.05).numpy()[0]
+    rec = m.stats[0]
+    assert rec['score_mean'] == float(fit.mean()) and rec['score_max'] == float(fit.max())
+    # a worker handed the list of batches scores the same
+    task = N.NESTask(batch_data=[{'fc_feats': b[0], 'gts': b[1]} for b in batches], noise_stdev=0.05, iteration=1)
+    res = N.EngineWorker(OracleEngine(dims, theta, fc, gts, df, n, table), spec, worker_id=1).fitness_batch(1, task, 0, P)
+    assert np.array_equal(np.stack([r.fitness for r in res]), fit)

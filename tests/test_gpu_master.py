@@ -35,7 +35,7 @@ class _Loader:
 def _spec(P):
     from nicnes import config as C
     exp = {'algorithm': 'nic_nes', 'nb_offspring': P,
-           'config': {'noise_stdev': 0.01, 'batch_size': 8, 'l2coeff': 1e-3, 'snapshot_freq': 0,
+           'config': {'noise_stdev': 0.01, 'batch_size': 8, 'l2coeff': 1e-3, 'snapshot_freq': 0, 'single_batch': True,
                       'schedule_start': 1, 'schedule_limit': 2, 'bs_multiplier': 2, 'stdev_divisor': 2,
                       'stepsize_divisor': 2},
            'policy_options': {'net': 'fc_caption', 'fitness': 'greedy', 'model_options': {}},

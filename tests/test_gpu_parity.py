@@ -385,3 +385,16 @@ def test_exact_tie_pass_matches_oracle(monkeypatch):
             assert _compare_tokens(seq[0, s], oseq, fr) == 0
     finally:
         e.close()
+
+
+@pytest.mark.parametrize('P', [2048, 8192, 1000], ids=['P2048', 'P8192', 'P1000_partial_chunk'])
+def test_rank_weights_bit_exact_large(eng, P):
+    """The sort-based rank (chunk bitonic sort + lower bounds) at configs[3]'s pop=2048 and beyond the
+    old one-workgroup cap; many ties, -0.0 / +0.0 and NaN (last, as numpy's argsort places it)."""
+    rng = np.random.default_rng(P)
+    fit = np.round(rng.random((P, 2)) * 200) / 4.0
+    fit[3, 0], fit[5, 1], fit[7, 0] = -0.0, 0.0, np.nan
+    cr, w = eng.rank_weights(torch.from_numpy(fit).cuda())
+    w_ref, cr_ref = O.weights_from_fitness(fit)
+    assert np.array_equal(cr.cpu().numpy(), cr_ref)
+    assert np.array_equal(w.cpu().numpy(), w_ref)
