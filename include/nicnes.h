@@ -104,6 +104,18 @@ int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, 
 int nicnes_noise_vectors(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
                          float* out, void* stream);
 
+/* Safe / proportional mutations (PolicyNet.evolve, src/algorithm/nets.py:96-113; Mutation enum :16-21):
+ * the member's noise becomes delta' = fp32(fp32(sigma * z) / vec) with mode NICNES_MUTATION_DIVIDE
+ * (SM-G-SUM, SM-G-ABS: vec = the sensitivity of src/algorithm/safe_mutations.py:93-147 after its
+ * underflow clamp and scaling; SM-VECTOR: the loaded vector, :25-29) or fp32(fp32(sigma * z) * vec)
+ * with NICNES_MUTATION_SCALE (SM-PROPORTIONAL: vec = |theta|, zeros replaced by mean |theta|).
+ * vec [D] fp32 device (copied). Every later evaluate / grad_partial / noise_vectors uses delta'
+ * (materialised per member, [max_members, D] on the device). NICNES_MUTATION_PLAIN turns it off. */
+#define NICNES_MUTATION_PLAIN 0
+#define NICNES_MUTATION_DIVIDE 1
+#define NICNES_MUTATION_SCALE 2
+int nicnes_set_mutation(nicnes_handle* h, int32_t mode, const float* vec, void* stream);
+
 /* Fitness criterion (Fitness enum + get_criterium, src/captioning/policies.py:22-61, applied at
  * :119-125): GREEDY = 100 * mean CIDEr-D; the greedy_* modes weight each step's probability of the
  * greedy token by the row's CIDEr-D (src/captioning/fitness.py:43-132). Other modes (sample,

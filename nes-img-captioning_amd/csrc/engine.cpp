@@ -78,6 +78,11 @@ struct nicnes_handle {
     int32_t* alive = nullptr;         // per decode workgroup: rows left unfinished (fused [stride], split [2][stride])
     int32_t alive_stride = 0;         // max decode workgroups (members x 64-row slabs)
     float* part = nullptr;            // split decode: partial greedy states
+    int mut_mode = 0;                 // nicnes_set_mutation: 0 plain, 1 divide, 2 multiply
+    float* mut_vec = nullptr;         // [D] sensitivity (mode 1) or |theta| scale (mode 2)
+    float* dbuf = nullptr;            // [max_members, Dp] the members' mutated deltas (mode != 0)
+    uint64_t* didx = nullptr;         // [max_members] k * Dp: row offsets of dbuf
+    int64_t Dp = 0;
     uint64_t* rank_key = nullptr;     // rank sort scratch (grown to the largest population ranked)
     uint32_t* rank_idx = nullptr;
     size_t rank_cap = 0;
@@ -330,7 +335,7 @@ int nicnes_destroy(nicnes_handle* h) {
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
                     h->ref_norm, h->nidx, h->seq, h->lp, h->row_scores, h->dscratch, h->stats, h->partials, h->norms,
                     h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive, h->part,
-                    h->rank_key, h->rank_idx, h->mbatch};
+                    h->rank_key, h->rank_idx, h->mbatch, h->mut_vec, h->dbuf, h->didx};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : h->ev)
@@ -523,7 +528,24 @@ int nicnes_noise_vectors(nicnes_handle* h, uint64_t iteration, int32_t member_be
     HIPC(h, hipSetDevice(h->device));
     HIPC(h, nicnes_launch_noise_index(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, h->cfg.noise_len,
                                       (uint64_t)h->D, h->nidx, s));
-    HIPC(h, nicnes_launch_noise_vectors(h->noise, h->nidx, count, h->D, sigma, out, s));
+    if (h->mut_mode)
+        HIPC(h, nicnes_launch_mutate(h->noise, h->nidx, count, h->D, sigma, h->mut_vec, h->mut_mode, out, h->D, s));
+    else
+        HIPC(h, nicnes_launch_noise_vectors(h->noise, h->nidx, count, h->D, sigma, out, s));
+    return NICNES_OK;
+}
+
+int nicnes_set_mutation(nicnes_handle* h, int32_t mode, const float* vec, void* stream) {
+    if (!h || mode < 0 || mode > 2 || (mode && !vec)) return NICNES_ERR_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    if (mode && !h->mut_vec) {       // first use: the [D] vector
+        HIPC(h, hipDeviceSynchronize());
+        int rc = dalloc(h, &h->mut_vec, (size_t)h->D);
+        if (rc) return rc;
+    }
+    if (mode) HIPC(h, hipMemcpyAsync(h->mut_vec, vec, (size_t)h->D * sizeof(float), hipMemcpyDeviceToDevice, s));
+    h->mut_mode = mode;
     return NICNES_OK;
 }
 
@@ -573,6 +595,20 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     p.theta = h->theta32;
     p.noise = h->noise;
     p.noise_idx = h->nidx;
+    if (h->mut_mode && !h->dbuf) {   // first mutated evaluation: [max_members, Dp] delta' rows
+        HIPC(h, hipDeviceSynchronize());
+        h->Dp = (h->D + 63) / 64 * 64;
+        int rc = dalloc(h, &h->dbuf, (size_t)h->cfg.max_members * (size_t)h->Dp);
+        if (!rc) rc = dalloc(h, &h->didx, (size_t)h->cfg.max_members);
+        if (rc) return rc;
+        HIPC(h, nicnes_launch_iota_stride(h->didx, h->cfg.max_members, (uint64_t)h->Dp, s));
+    }
+    if (h->mut_mode) {      // safe / proportional mutations: the decode reads the members' delta' with sigma 1
+        HIPC(h, nicnes_launch_mutate(h->noise, h->nidx, count, h->D, sigma, h->mut_vec, h->mut_mode, h->dbuf, h->Dp, s));
+        p.noise = h->dbuf;
+        p.noise_idx = h->didx;
+        sigma = 1.0f;
+    }
     p.fc = h->fc;
     p.member_batch = mb;
     p.seq = seq_out ? seq_out : h->seq;
@@ -654,7 +690,9 @@ int nicnes_grad_partial(nicnes_handle* h, uint64_t iteration, int32_t member_beg
     HIPC(h, hipSetDevice(h->device));
     HIPC(h, nicnes_launch_noise_index(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, h->cfg.noise_len,
                                       (uint64_t)h->D, h->nidx, s));
-    HIPC(h, nicnes_launch_grad(h->noise, h->nidx, w, count, sigma, h->D, gsum_out, s));
+    // with a mutation the reference sums the mutated noise vectors it was sent (nic_nes_worker.py:156-161):
+    // the kernel transforms each delta on the fly
+    HIPC(h, nicnes_launch_grad(h->noise, h->nidx, w, count, sigma, h->D, h->mut_vec, h->mut_mode, gsum_out, s));
     return NICNES_OK;
 }
 

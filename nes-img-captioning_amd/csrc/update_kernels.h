@@ -28,10 +28,14 @@ extern "C" hipError_t nicnes_launch_noise_index(uint64_t seed, uint64_t iteratio
                                                 uint64_t table_len, uint64_t dim, uint64_t* out, hipStream_t s);
 extern "C" hipError_t nicnes_launch_noise_vectors(const float* noise, const uint64_t* idx, int count, int64_t dim,
                                                   float sigma, float* out, hipStream_t s);
+extern "C" hipError_t nicnes_launch_mutate(const float* noise, const uint64_t* idx, int count, int64_t dim, float sigma,
+                                           const float* vec, int mode, float* out, int64_t out_stride, hipStream_t s);
+extern "C" hipError_t nicnes_launch_iota_stride(uint64_t* out, int n, uint64_t stride, hipStream_t s);
 extern "C" size_t nicnes_rank_scratch_pairs(int n);
 extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, uint64_t* skey, uint32_t* sidx, double* cr_out,
                                          float* w_out, hipStream_t s);
+// mode 0: delta = fp32(sigma * z); 1: delta / vec[j]; 2: delta * vec[j] (safe / proportional mutations)
 extern "C" hipError_t nicnes_launch_grad(const float* noise, const uint64_t* idx, const float* w, int count, float sigma,
-                                         int64_t dim, float* gsum, hipStream_t s);
+                                         int64_t dim, const float* vec, int mode, float* gsum, hipStream_t s);
 extern "C" int nicnes_adam_blocks(int64_t dim);
 extern "C" hipError_t nicnes_launch_adam(const AdamParams* p, double* norms_out, hipStream_t s);

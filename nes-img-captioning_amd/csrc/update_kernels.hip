@@ -106,26 +106,43 @@ __global__ __launch_bounds__(256) void nicnes_rank_kernel(const double* fit, int
     w_out[p] = (float)(cr[0] - cr[1]);         // cr[:, 0] - cr[:, 1], then fp32 (gradient_estimate)
 }
 
-// gsum[j] = fp32( sum_i w_i * fp32(sigma * z[idx_i + j]) ), fp64 accumulation in member order
+// gsum[j] = fp32( sum_i w_i * delta_i[j] ), fp64 accumulation in member order, with
+// delta_i[j] = fp32(sigma * z[idx_i + j]) transformed by the mutation MODE (0 none, 1 / v[j], 2 * v[j]):
+// safe / proportional mutations are applied on the fly, the per-member deltas are never stored
+template <int MODE>
+__device__ __forceinline__ float grad_delta(float sigma, float z, float v) {
+    const float d = sigma * z;
+    return MODE == 1 ? d / v : (MODE == 2 ? d * v : d);
+}
+
+template <int MODE>
 __global__ __launch_bounds__(256) void nicnes_grad_kernel(const float* noise, const uint64_t* idx, const float* w,
-                                                          int count, float sigma, int64_t dim, float* gsum) {
+                                                          int count, float sigma, int64_t dim, const float* vec,
+                                                          float* gsum) {
     const int64_t j4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     if (j4 >= dim) return;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     const bool full = j4 + 4 <= dim;
+    f32x4 v = {1.f, 1.f, 1.f, 1.f};
+    if (MODE) {
+        if (full) v = *reinterpret_cast<const f32x4*>(vec + j4);
+        else
+            for (int q = 0; q < 3; ++q)
+                if (j4 + q < dim) v[q] = vec[j4 + q];
+    }
     for (int i = 0; i < count; ++i) {
         const float* z = noise + idx[i] + j4;
         const double wi = (double)w[i];
         if (full) {
             const f32x4 zz = *reinterpret_cast<const f32x4*>(z);
-            a0 += wi * (double)(sigma * zz[0]);
-            a1 += wi * (double)(sigma * zz[1]);
-            a2 += wi * (double)(sigma * zz[2]);
-            a3 += wi * (double)(sigma * zz[3]);
+            a0 += wi * (double)grad_delta<MODE>(sigma, zz[0], v[0]);
+            a1 += wi * (double)grad_delta<MODE>(sigma, zz[1], v[1]);
+            a2 += wi * (double)grad_delta<MODE>(sigma, zz[2], v[2]);
+            a3 += wi * (double)grad_delta<MODE>(sigma, zz[3], v[3]);
         } else {
-            a0 += wi * (double)(sigma * z[0]);
-            if (j4 + 1 < dim) a1 += wi * (double)(sigma * z[1]);
-            if (j4 + 2 < dim) a2 += wi * (double)(sigma * z[2]);
+            a0 += wi * (double)grad_delta<MODE>(sigma, z[0], v[0]);
+            if (j4 + 1 < dim) a1 += wi * (double)grad_delta<MODE>(sigma, z[1], v[1]);
+            if (j4 + 2 < dim) a2 += wi * (double)grad_delta<MODE>(sigma, z[2], v[2]);
         }
     }
     gsum[j4] = (float)a0;
@@ -243,10 +260,15 @@ extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, uint64_t* ske
 }
 
 extern "C" hipError_t nicnes_launch_grad(const float* noise, const uint64_t* idx, const float* w, int count, float sigma,
-                                         int64_t dim, float* gsum, hipStream_t s) {
+                                         int64_t dim, const float* vec, int mode, float* gsum, hipStream_t s) {
     const int64_t n4 = (dim + 3) / 4;
-    hipLaunchKernelGGL(nicnes_grad_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, noise, idx, w, count,
-                       sigma, dim, gsum);
+    const dim3 grid((unsigned)((n4 + 255) / 256));
+    if (mode == 1)
+        hipLaunchKernelGGL(nicnes_grad_kernel<1>, grid, dim3(256), 0, s, noise, idx, w, count, sigma, dim, vec, gsum);
+    else if (mode == 2)
+        hipLaunchKernelGGL(nicnes_grad_kernel<2>, grid, dim3(256), 0, s, noise, idx, w, count, sigma, dim, vec, gsum);
+    else
+        hipLaunchKernelGGL(nicnes_grad_kernel<0>, grid, dim3(256), 0, s, noise, idx, w, count, sigma, dim, vec, gsum);
     return hipGetLastError();
 }
 
@@ -265,6 +287,39 @@ __global__ __launch_bounds__(256) void nicnes_noise_vectors_kernel(const float* 
 extern "C" hipError_t nicnes_launch_noise_vectors(const float* noise, const uint64_t* idx, int count, int64_t dim,
                                                   float sigma, float* out, hipStream_t s) {
     hipLaunchKernelGGL(nicnes_noise_vectors_kernel, dim3(512, count), dim3(256), 0, s, noise, idx, dim, sigma, out);
+    return hipGetLastError();
+}
+
+// Safe / proportional mutations (src/algorithm/nets.py:96-113): delta'_k = fp32(fp32(sigma * z) / vec)
+// (mode 1: SM-G-SUM, SM-G-ABS, SM-VECTOR divide the noise by the sensitivity) or fp32(fp32(sigma * z) *
+// vec) (mode 2: SM-PROPORTIONAL multiplies it by |theta|), IEEE division as torch's in-place /=.
+// out row k at out + k * out_stride.
+__global__ __launch_bounds__(256) void nicnes_mutate_kernel(const float* noise, const uint64_t* idx, int64_t dim,
+                                                            float sigma, const float* vec, int mode, float* out,
+                                                            int64_t out_stride) {
+    const int k = blockIdx.y;
+    const float* z = noise + idx[k];
+    float* o = out + (size_t)k * out_stride;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < dim; j += (int64_t)gridDim.x * blockDim.x) {
+        const float d = sigma * z[j];
+        o[j] = mode == 1 ? d / vec[j] : d * vec[j];
+    }
+}
+
+extern "C" hipError_t nicnes_launch_mutate(const float* noise, const uint64_t* idx, int count, int64_t dim, float sigma,
+                                           const float* vec, int mode, float* out, int64_t out_stride, hipStream_t s) {
+    hipLaunchKernelGGL(nicnes_mutate_kernel, dim3(512, count), dim3(256), 0, s, noise, idx, dim, sigma, vec, mode, out,
+                       out_stride);
+    return hipGetLastError();
+}
+
+__global__ void nicnes_iota_stride_kernel(uint64_t* out, int n, uint64_t stride) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (uint64_t)i * stride;
+}
+
+extern "C" hipError_t nicnes_launch_iota_stride(uint64_t* out, int n, uint64_t stride, hipStream_t s) {
+    hipLaunchKernelGGL(nicnes_iota_stride_kernel, dim3((n + 255) / 256), dim3(256), 0, s, out, n, stride);
     return hipGetLastError();
 }
 

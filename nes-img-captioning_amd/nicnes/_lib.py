@@ -19,7 +19,7 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_optimizer_update', 'nicnes_last_ratio', 'nicnes_set_fitness_mode', 'nicnes_evaluate_lp',
            'nicnes_set_decode_split', 'nicnes_decode_shape', 'nicnes_comm_unique_id', 'nicnes_comm_init',
            'nicnes_comm_attach', 'nicnes_comm_destroy', 'nicnes_allgather_fitness', 'nicnes_allreduce_grad',
-           'nicnes_noise_vectors', 'nicnes_set_batches', 'nicnes_evaluate_batches']
+           'nicnes_noise_vectors', 'nicnes_set_batches', 'nicnes_evaluate_batches', 'nicnes_set_mutation']
 
 
 class NicnesConfig(ctypes.Structure):
@@ -67,6 +67,7 @@ def lib(path=None):
         'nicnes_set_fitness_mode': (c.c_int, [vp, i32]),
         'nicnes_noise_vectors': (c.c_int, [vp, u64, i32, i32, f32, vp, vp]),
         'nicnes_set_batches': (c.c_int, [vp, vp, i32, i32, vp, i32, vp, vp]),
+        'nicnes_set_mutation': (c.c_int, [vp, i32, vp, vp]),
         'nicnes_evaluate_batches': (c.c_int, [vp, u64, i32, i32, f32, vp, vp, vp, vp, vp]),
         'nicnes_rank_weights': (c.c_int, [vp, vp, i32, vp, vp, vp]),
         'nicnes_grad_partial': (c.c_int, [vp, u64, i32, i32, vp, f32, vp, vp]),

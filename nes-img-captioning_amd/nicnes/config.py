@@ -7,9 +7,9 @@ Field names and defaults mirror
   optimizer_options /root/reference/src/algorithm/nic_nes/experiment.py:20-21
 A leading underscore disables a key ("_from_infos"), as in the reference JSON files. The engine
 implements the mscoco_nes.json hot path only: net 'fc_caption', fitness 'greedy' or one of the
-greedy_* criteria (greedy_logprob / expprob / linprob / avgprob), no vbn /
-layer_n / safe mutations; anything else raises NotSupported (nicnes_create returns
-NICNES_ERR_UNSUPPORTED for unsupported model sizes).
+greedy_* criteria (greedy_logprob / expprob / linprob / avgprob), model_options.safe_mutations
+'' / SM-G-SUM / SM-VECTOR / SM-PROPORTIONAL (nicnes.mutations), no vbn / layer_n; anything else
+raises NotSupported (nicnes_create returns NICNES_ERR_UNSUPPORTED for unsupported model sizes).
 """
 import json
 from collections import namedtuple
@@ -86,14 +86,24 @@ class ExperimentSpec:
                                % (po.fitness, ', '.join(GREEDY_FITNESS)))
         if po.vbn or mo.vbn_e or mo.layer_n:
             raise NotSupported('virtual batch norm / layer norm are not implemented by the engine')
-        if (po.safe_mutations or '') or (mo.safe_mutations or ''):
-            raise NotSupported('safe mutations are not implemented by the engine')
+        m = self.mutation
+        if m == 'SM-G-ABS':
+            raise NotSupported("SM-G-ABS: the reference's _calc_abs_sensitivity raises AttributeError "
+                               "(self.nb_params on Sensitivity, safe_mutations.py:125)")
+        if m not in ('', 'SM-G-SUM', 'SM-VECTOR', 'SM-PROPORTIONAL'):
+            raise NotSupported('safe_mutations %r (Mutation, src/algorithm/nets.py:16-21)' % m)
 
     # ------------------------------------------------------------------------------------
     @property
     def fitness(self):
         """policy_options.fitness; Fitness.DEFAULT is 'greedy' (policies.py:35)."""
         return self.policy_options.fitness or 'greedy'
+
+    @property
+    def mutation(self):
+        """model_options.safe_mutations: the option the network reads (Mutation(options.safe_mutations),
+        nets.py:46); policy_options.safe_mutations is not read by the reference's nets."""
+        return self.model_options.safe_mutations or ''
 
     @property
     def single_batch(self):

@@ -178,6 +178,21 @@ class Engine:
                                               ctypes.c_float(sigma), _ptr(o), self._stream()), self.h, 'noise_vectors')
         return o
 
+    MUTATION_MODES = {'plain': 0, 'divide': 1, 'scale': 2}
+
+    def set_mutation(self, mode='plain', vec=None):
+        """Per-parameter noise transform of safe / proportional mutations: 'divide' (delta / vec:
+        SM-G-SUM, SM-G-ABS, SM-VECTOR with vec = the sensitivity), 'scale' (delta * vec:
+        SM-PROPORTIONAL), 'plain' off."""
+        code = self.MUTATION_MODES[mode] if isinstance(mode, str) else int(mode)
+        v = self._dev(vec, torch.float32) if vec is not None else None
+        if v is not None and v.numel() != self.D:
+            raise ValueError('mutation vector needs D entries')
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_set_mutation(self.h, code, _ptr(v), self._stream()), self.h, 'set_mutation')
+        self._keep['mutation'] = v
+        self.mutation_mode = code
+
     # Fitness enum values the engine implements (src/captioning/policies.py:22-35) -> nicnes.h codes
     FITNESS_MODES = {'greedy': 0, 'greedy_logprob': 1, 'greedy_expprob': 2, 'greedy_linprob': 3,
                      'greedy_avgprob': 4}

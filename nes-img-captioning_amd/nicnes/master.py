@@ -89,6 +89,18 @@ class EngineMaster:
         self.stats = []
         self._batch_key = None
         self._n_batches = 1
+        self.mutator = None
+        if spec.mutation:
+            from .mutations import Mutator
+            self.mutator = Mutator(spec, engine)
+
+    def _prepare_mutation(self, batch):
+        """Safe / proportional mutations: the iteration's noise transform, computed from the fp32 theta
+        the members evaluate and the iteration's (first) batch, the vector the workers compute
+        (nicnes.mutations)."""
+        if self.mutator is not None and self.mutator.active:
+            from .mutations import batch_fc
+            self.mutator.prepare(self.sched.iteration, self.e.theta()[1], batch_fc(batch))
 
     # ------------------------------------------------------------------------ helpers ----------
     def _set_batch(self, batch):
@@ -163,6 +175,7 @@ class EngineMaster:
                 t0 = time.time()
                 self.sched.incr_iteration()
                 self._set_batch(batch)
+                self._prepare_mutation(batch)
                 if runner is None or runner.sigma != self.sched.noise_stdev:
                     runner = PopulationRunner(self.e, P, self.sched.noise_stdev, rank=self.rank,
                                               world_size=self.world, group=self.group, comm=self.comm)
@@ -210,6 +223,7 @@ class EngineMaster:
             t0 = time.time()
             self.sched.incr_iteration()
             self._set_batch(batch)
+            self._prepare_mutation(batch)
             sigma = self.sched.noise_stdev
             task_id = client.declare_task(NESTask(current=self.serialize_current(), batch_data=batch,
                                                   noise_stdev=sigma, batch_size=self.sched.batch_size,

@@ -168,6 +168,10 @@ class EngineWorker:
         self.spec = spec
         self.worker_id = worker_id if worker_id is not None else os.getpid()
         self.policy = EnginePolicy(engine, spec)
+        self.mutator = None
+        if spec is not None and spec.mutation:
+            from .mutations import Mutator
+            self.mutator = Mutator(spec, engine)
 
     def _prepare(self, task_id, task_data):
         # theta and batch are loaded once per task (the reference reloads them per member)
@@ -180,6 +184,10 @@ class EngineWorker:
             self._cur = (task_id, cur)
         if task_data.batch_data is not None:
             self.policy._ensure_batch(task_data.batch_data)
+        if self.mutator is not None and self.mutator.active:
+            # calc_sensitivity of the task's theta on its batch before evolve (nic_nes_worker.py:137-142)
+            from .mutations import batch_fc
+            self.mutator.prepare((task_id, getattr(self, '_cur', None)), self.e.theta()[1], batch_fc(task_data.batch_data))
 
     def fitness_batch(self, task_id, task_data, member_begin, count):
         """-> list of NESResult(fitness=[f+, f-] fp64, noise_idx, member)."""

@@ -132,10 +132,21 @@ def noise_table(table_len, seed=123):
     return np.random.Generator(np.random.PCG64(seed)).standard_normal(table_len, dtype=np.float32)
 
 
-def perturb(theta32, table, idx, sigma, sign):
-    """delta = fp32(sigma * z) (nets.py:102 draws N(0, sigma) in fp32); theta +/- delta in fp32
-    (nets.py:113, nic_nes_worker.py:151)."""
-    delta = np.float32(sigma) * table[idx: idx + theta32.size]
+def member_delta(table, idx, sigma, dim, mutation=None):
+    """delta = fp32(sigma * z) (nets.py:102 draws N(0, sigma) in fp32), then the mutation transform
+    of nets.py:104-112 in fp32: ('divide', s) -> delta / s (SM-G-SUM / SM-VECTOR), ('scale', a) ->
+    delta * a (SM-PROPORTIONAL, a = |theta'|)."""
+    delta = np.float32(sigma) * table[idx: idx + dim]
+    if mutation is not None and mutation[0] != 'plain':
+        mode, vec = mutation
+        vec = np.asarray(vec, np.float32)
+        delta = (delta / vec) if mode == 'divide' else (delta * vec)
+    return delta.astype(np.float32)
+
+
+def perturb(theta32, table, idx, sigma, sign, mutation=None):
+    """theta +/- delta in fp32 (nets.py:113, nic_nes_worker.py:151)."""
+    delta = member_delta(table, idx, sigma, theta32.size, mutation)
     return (theta32 + delta) if sign > 0 else (theta32 - delta)
 
 
@@ -195,14 +206,13 @@ def weights_from_fitness(fitness):
     return (cr[:, 0] - cr[:, 1]).astype(np.float32), cr
 
 
-def gradient(fitness, table, indices, sigma, dim):
+def gradient(fitness, table, indices, sigma, dim, mutation=None):
     """nic_nes_master.py:170-182: g = sum_i w_i * delta_i / (2F). The engine accumulates in fp64
     in member order and rounds once to fp32 (the reference accumulates in fp32 BLAS order)."""
     w, _ = weights_from_fitness(fitness)
     acc = np.zeros(dim, np.float64)
-    s = np.float32(sigma)
     for i, idx in enumerate(indices):
-        delta = s * table[int(idx): int(idx) + dim]
+        delta = member_delta(table, int(idx), sigma, dim, mutation)
         acc += np.float64(w[i]) * delta.astype(np.float64)
     g = acc.astype(np.float32)
     g /= np.float32(2 * len(indices))

@@ -33,6 +33,11 @@ Fixtures (all .npz, loadable with allow_pickle=False):
                                   it (a batch dict of numpy arrays / lists / dicts), of (task_id, NESResult) as
                                   a worker pushes it (nic_nes_worker.py:156-161, dist.py:199-201), and of an
                                   experiment dict (dist.py:73-76)
+  mutations.npz                   PolicyNet.evolve with safe / proportional mutations (src/algorithm/nets.py:83-119):
+                                  the raw normal_ draw, the returned noise (raw / sensitivity, raw * |theta'|)
+                                  for SM-G-SUM with a set sensitivity and for SM-PROPORTIONAL; and the SM-G-SUM
+                                  sensitivity itself, Sensitivity.calc_sensitivity (safe_mutations.py:34-117)
+                                  on a tiny FCModel through forward_for_sensitivity (captioning/nets.py:22-70)
   fitness_criteria.npz            the greedy_* fitness criteria (src/captioning/fitness.py:43-132, chosen
                                   by Fitness.get_criterium, src/captioning/policies.py:50-61) on seeded
                                   logprobs / sequences / per-row CIDEr rewards, as CaptPolicy.rollout
@@ -239,6 +244,38 @@ def wire_fixture():
     print('wire: task %d B, result %d B' % (len(serialize(task)), len(serialize((7, result)))))
 
 
+def mutations_fixture():
+    import tempfile
+    d = O.Dims(vocab_size=63, E=32, R=32, F=64)
+    B = 4
+    theta = O.make_theta(d, 5, 4.0, 0.0)                  # zero biases: SM-PROPORTIONAL's mean replacement
+    fc = np.random.Generator(np.random.PCG64(66)).standard_normal((B, d.F)).astype(np.float32)
+
+    def model(mode, underflow=0.1):
+        opt = Opt(d.vocab_size, d.E, d.R, d.F, False, False, False, False, False, mode, underflow, '')
+        m = ref_nets.FCModel(options=opt)
+        load_theta(m, theta)
+        return m
+    # SM-G-SUM sensitivity on the batch (5 duplicated rows per image, as the loader gives)
+    m = model('SM-G-SUM', 0.1)
+    with tempfile.TemporaryDirectory() as tmp:
+        m.calc_sensitivity(0, 0, {'fc_feats': np.repeat(fc, 5, axis=0)}, B, tmp)
+    sens = m.get_sensitivity_vector().numpy().astype(np.float32)
+    # evolve with that sensitivity
+    torch.manual_seed(11)
+    raw = torch.empty(d.D).normal_(mean=0.0, std=0.01).numpy()
+    torch.manual_seed(11)
+    delta_safe = m.evolve(0.01)
+    # SM-PROPORTIONAL
+    mp_ = model('SM-PROPORTIONAL')
+    torch.manual_seed(11)
+    delta_prop = mp_.evolve(0.01)
+    np.savez_compressed(os.path.join(OUT, 'mutations.npz'), theta=theta, fc=fc, dims=np.array([d.vocab_size, d.E, d.R, d.F]),
+                        underflow=np.float64(0.1), sensitivity=sens, raw=raw, delta_safe=delta_safe,
+                        delta_prop=delta_prop)
+    print('mutations: sens min %.3g max %.3g' % (sens.min(), sens.max()))
+
+
 def perturb_fixture():
     d = O.Dims(vocab_size=63, E=32, R=32, F=64)
     model = ref_model(d)
@@ -364,6 +401,7 @@ def all_fixtures():
     decode_bench_fixture()
     master_ranks_grad_fixture()
     wire_fixture()
+    mutations_fixture()
 
 
 if __name__ == '__main__':

@@ -25,6 +25,11 @@ class OracleEngine:
         self.theta32 = theta32.copy()
         self.theta_src = theta32.copy()
         self.fitness_mode = 0
+        self.mutation = None
+
+    def set_mutation(self, mode='plain', vec=None):
+        v = vec.numpy() if isinstance(vec, torch.Tensor) else vec
+        self.mutation = None if mode == 'plain' else (mode, np.asarray(v, np.float32).copy())
 
     def set_fitness_mode(self, fitness):
         self.fitness_mode = CR.CRITERIA[fitness] if isinstance(fitness, str) else int(fitness)
@@ -51,8 +56,7 @@ class OracleEngine:
         return torch.tensor([self._idx(iteration, member_begin + k) for k in range(count)], dtype=torch.int64)
 
     def noise_vectors(self, iteration, member_begin, count, sigma, out=None):
-        s = np.float32(sigma)
-        v = np.stack([s * self.table[self._idx(iteration, member_begin + k): self._idx(iteration, member_begin + k) + self.D]
+        v = np.stack([O.member_delta(self.table, self._idx(iteration, member_begin + k), sigma, self.D, self.mutation)
                       for k in range(count)])
         return torch.from_numpy(v)
 
@@ -81,7 +85,7 @@ class OracleEngine:
             idx = self._idx(iteration, member_begin + k)
             fc, gts = (self.fc, self.gts) if member_batch is None else self.batches[member_batch[k]]
             for s, sign in enumerate((+1, -1)):
-                seq, lp, _ = O.decode(self.dims, O.perturb(self.theta32, self.table, idx, sigma, sign), fc)
+                seq, lp, _ = O.decode(self.dims, O.perturb(self.theta32, self.table, idx, sigma, sign, self.mutation), fc)
                 f, scores = CR.rollout_fitness(self.scorer, seq, gts)
                 out[k, s] = CR.criterion_fitness(self.fitness_mode, lp, seq, scores) if self.fitness_mode else f
         return out
@@ -92,10 +96,10 @@ class OracleEngine:
 
     def grad_partial(self, iteration, member_begin, count, w_shard, sigma, out=None):
         acc = np.zeros(self.D, np.float64)
-        s = np.float32(sigma)
         for k in range(count):
             idx = self._idx(iteration, member_begin + k)
-            acc += np.float64(w_shard[k].item()) * (s * self.table[idx: idx + self.D]).astype(np.float64)
+            acc += np.float64(w_shard[k].item()) * O.member_delta(self.table, idx, sigma, self.D,
+                                                                  self.mutation).astype(np.float64)
         g = torch.from_numpy(acc.astype(np.float32))
         if out is not None:
             out.copy_(g)

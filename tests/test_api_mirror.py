@@ -59,7 +59,8 @@ def test_spec_reads_mscoco_nes():
     {'policy_options': {'net': 'fc_caption', 'fitness': 'sample'}},
     {'policy_options': {'net': 'att_caption'}},
     {'policy_options': {'net': 'fc_caption', 'vbn': True}},
-    {'policy_options': {'net': 'fc_caption', 'model_options': {'safe_mutations': 'SM-G-SUM'}}},
+    {'policy_options': {'net': 'fc_caption', 'model_options': {'safe_mutations': 'SM-G-ABS'}}},
+    {'policy_options': {'net': 'fc_caption', 'model_options': {'safe_mutations': 'SM-OTHER'}}},
     {'optimizer_options': {'type': 'rmsprop', 'args': {}}},
     {'algorithm': 'nic_es'},
 ])
@@ -386,3 +387,68 @@ def test_per_member_batches_single_batch_false():
     task = N.NESTask(batch_data=[{'fc_feats': b[0], 'gts': b[1]} for b in batches], noise_stdev=0.05, iteration=1)
     res = N.EngineWorker(OracleEngine(dims, theta, fc, gts, df, n, table), spec, worker_id=1).fitness_batch(1, task, 0, P)
     assert np.array_equal(np.stack([r.fitness for r in res]), fit)
+
+
+# ------------------------------------------------------------------ safe / proportional mutations ----
+def _mut_spec(P, mode, **mo):
+    return C.ExperimentSpec(_exp(nb_offspring=P, config={'noise_stdev': 0.05, 'batch_size': 4, 'l2coeff': 1e-3,
+                                                         'snapshot_freq': 0},
+                                 policy_options={'net': 'fc_caption', 'fitness': 'greedy',
+                                                 'model_options': dict(safe_mutations=mode, **mo)},
+                                 optimizer_options={'type': 'adam', 'args': {'stepsize': 0.01}}), vocab_size=63)
+
+
+def test_mutation_goldens_from_the_reference():
+    """tests/golden/mutations.npz (scripts/make_golden.py, the reference's FCModel): the host SM-G-SUM
+    sensitivity equals Sensitivity.calc_sensitivity bit for bit; the oracle's transform of a noise draw
+    equals PolicyNet.evolve's returned noise for SM-G-SUM and SM-PROPORTIONAL."""
+    from nicnes import mutations as MU
+    g = np.load('tests/golden/mutations.npz')
+    V, E, R, F_ = [int(x) for x in g['dims']]
+    s = MU.clamp_calc(MU.sum_sensitivity((V + 1, E, R, F_), g['theta'], g['fc'], 4), float(g['underflow']))
+    assert np.array_equal(s.numpy(), g['sensitivity'])
+    raw = g['raw']
+    D = raw.size
+    assert np.array_equal(O.member_delta(raw, 0, 1.0, D, ('divide', g['sensitivity'])), g['delta_safe'])
+    prop = MU.proportional_vector(g['theta']).numpy()
+    assert (g['theta'] == 0).sum() > 0 and np.array_equal(O.member_delta(raw, 0, 1.0, D, ('scale', prop)),
+                                                          g['delta_prop'])
+
+
+def test_mutation_vector_file(tmp_path):
+    """Sensitivity.set_sensitivity (safe_mutations.py:27-31): clamp at the underflow, divide by the min."""
+    from nicnes import mutations as MU
+    v = torch.tensor([0.01, 0.5, 2.0, 0.05, 1.0])
+    torch.save(v, str(tmp_path / 'sens.pt'))
+    got = MU.load_vector_file(str(tmp_path / 'sens.pt'), 0.1)
+    want = torch.tensor([0.1, 0.5, 2.0, 0.1, 1.0]) / 0.1
+    assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize('mode', ['SM-G-SUM', 'SM-PROPORTIONAL'])
+def test_mutation_dispatched_loop_matches_local_loop(workload, tmp_path, mode):
+    """Workers (EngineWorker._prepare) and the master (_prepare_mutation) compute the same vector, so the
+    dispatched loop's update equals the local loop's; and the mutation changes the trajectory."""
+    dims, theta, fc, gts, df, n, table = workload
+    P, iters = 4, 2
+    batch = {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts}
+    spec = _mut_spec(P, mode, safe_mutation_underflow=0.1)
+    local = M.EngineMaster(spec, _engine(workload), log_dir=str(tmp_path / 'a'))
+    local.run([batch], max_iterations=iters)
+    assert local.e.mutation is not None and local.e.mutation[0] == ('divide' if mode == 'SM-G-SUM' else 'scale')
+    plain = M.EngineMaster(_spec(P), _engine(workload), log_dir=str(tmp_path / 'c'))
+    plain.run([batch], max_iterations=iters)
+    assert not np.array_equal(plain.e.theta()[0].numpy(), local.e.theta()[0].numpy())
+
+    e_master, e_worker = _engine(workload), _engine(workload)
+    master = M.EngineMaster(spec, e_master, log_dir=str(tmp_path / 'b'))
+    store = T.LocalStore()
+    worker = N.EngineWorker(e_worker, spec, worker_id=1)
+    th = threading.Thread(target=M.run_worker, args=(T.WorkerClient(store), worker),
+                          kwargs=dict(chunk=4, max_tasks=iters), daemon=True)
+    th.start()
+    master.run_dispatched(T.MasterClient(store), [batch] * iters, max_iterations=iters, result_timeout=120)
+    th.join(timeout=120)
+    assert not th.is_alive()
+    assert np.array_equal(local.e.theta()[0].numpy(), master.e.theta()[0].numpy())
+    assert np.array_equal(e_worker.mutation[1], e_master.mutation[1])

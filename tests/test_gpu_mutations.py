@@ -1,0 +1,123 @@
+"""Safe / proportional mutations on the GPU (PolicyNet.evolve, src/algorithm/nets.py:83-119): with
+nicnes_set_mutation the members evaluate theta +/- delta', delta' = fp32(sigma * z) / s (SM-G-SUM,
+SM-VECTOR) or fp32(sigma * z) * |theta'| (SM-PROPORTIONAL), and the weighted noise sum and
+nicnes_noise_vectors use the same delta'. Checked against the oracle (oracle.member_delta):
+tokens and CIDEr-D fitness of every member on the fused and the split decode, delta' bit for bit,
+the noise sum bit for bit (fp64 accumulation in member order, one rounding)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O          # noqa: E402
+from oracle import cider_ref as CR      # noqa: E402
+
+NOISE_LEN = 1 << 23
+SIGMA = 0.01
+SEED, IT = 6, 9
+
+
+def _vector(mode, theta, D):
+    from nicnes import mutations as MU
+    if mode == 'scale':
+        return MU.proportional_vector(theta).numpy()
+    # a sensitivity-like vector: clamped at the underflow and divided by it (values >= 1)
+    s = np.random.Generator(np.random.PCG64(5)).gamma(0.5, 4.0, D).astype(np.float32)
+    return MU.clamp_calc(torch.from_numpy(s), 0.1).numpy()
+
+
+@pytest.mark.parametrize('shape', [(1, 4), (4, 2)], ids=['fused', 'split_G2S4'])
+@pytest.mark.parametrize('mode', ['divide', 'scale'])
+def test_mutated_members_match_oracle(mode, shape):
+    import nicnes
+    import nicnes.synthetic as S
+    dims = O.Dims()
+    theta = O.make_theta(dims, 4, 4.0, 0.1)
+    theta[:dims.E * dims.F:7] = 0.0                      # exact zeros: SM-PROPORTIONAL's mean replacement
+    B, P = 24, 5
+    fc = np.random.Generator(np.random.PCG64(31)).standard_normal((B, dims.F)).astype(np.float32)
+    base, _, _ = O.decode(dims, theta, fc)
+    gts, df, n = S.build_references(base, dims.vocab_size, seed=3, n_refs=5, df_sets=128)
+    table = O.noise_table(NOISE_LEN, 123)
+    vec = _vector(mode, theta, dims.D)
+    mut = (mode, vec)
+    e = nicnes.Engine(max_batch=B, max_members=P, noise_len=NOISE_LEN, noise_seed=SEED)
+    try:
+        e.set_noise_table(table)
+        keys, vals = nicnes.df_table_arrays(df)
+        e.set_df_table(keys, vals, np.log(float(n)))
+        e.set_theta(theta)
+        e.set_batch(fc, gts)
+        e.set_decode_split(*shape)
+        e.set_mutation(mode, vec)
+        fit, seq = e.evaluate(IT, 0, P, SIGMA, return_seq=True)
+        fit, seq = fit.cpu().numpy(), seq.cpu().numpy()
+        dv = e.noise_vectors(IT, 0, P, SIGMA).cpu().numpy()
+        scorer = CR.CiderDOracle(df, n)
+        idx = [O.noise_index(SEED, IT, k, NOISE_LEN, dims.D) for k in range(P)]
+        for k in range(P):
+            want = O.member_delta(table, idx[k], SIGMA, dims.D, mut)
+            assert np.array_equal(dv[k], want), k
+            assert not np.array_equal(want, O.member_delta(table, idx[k], SIGMA, dims.D))
+            for s, sign in enumerate((+1, -1)):
+                oseq, _, fr = O.decode(dims, O.perturb(theta, table, idx[k], SIGMA, sign, mut), fc)
+                ok = fr.any(axis=1) | (seq[k, s] == oseq).all(axis=1)
+                assert ok.all(), (k, s)
+                if not fr.any():
+                    f_ref = CR.rollout_fitness(scorer, oseq, gts)[0]
+                    assert abs(fit[k, s] - f_ref) <= 1e-9 * max(1.0, f_ref), (k, s, fit[k, s], f_ref)
+        w = torch.linspace(-0.5, 0.5, P, dtype=torch.float32, device=e.device)
+        g = e.grad_partial(IT, 0, P, w, SIGMA).cpu().numpy()
+        acc = np.zeros(dims.D, np.float64)
+        for k in range(P):
+            acc += np.float64(w[k].item()) * O.member_delta(table, idx[k], SIGMA, dims.D, mut).astype(np.float64)
+        assert np.array_equal(g, acc.astype(np.float32))
+        # plain again: the table's delta
+        e.set_mutation('plain')
+        dv0 = e.noise_vectors(IT, 0, 1, SIGMA).cpu().numpy()
+        assert np.array_equal(dv0[0], np.float32(SIGMA) * table[idx[0]: idx[0] + dims.D])
+    finally:
+        e.close()
+
+
+def test_safe_mutation_master_trajectory_matches_oracle_engine():
+    """EngineMaster.run with model_options.safe_mutations 'SM-G-SUM': the host sensitivity (nicnes.mutations,
+    pinned to the reference by tests/golden/mutations.npz) drives the GPU transform; two iterations
+    match the oracle engine run by the same master."""
+    import nicnes
+    import nicnes.synthetic as S
+    from nicnes import config as C, master as M
+    from tests.cpu_engine import OracleEngine
+    dims = O.Dims()
+    theta = O.make_theta(dims, 0, 4.0, 0.1)
+    fc = np.random.Generator(np.random.PCG64(1234)).standard_normal((8, dims.F)).astype(np.float32)
+    base, _, _ = O.decode(dims, theta, fc)
+    gts, df, n = S.build_references(base, dims.vocab_size, seed=9, n_refs=5, df_sets=128)
+    table = O.noise_table(NOISE_LEN, 123)
+    P = 4
+    spec = C.ExperimentSpec({'algorithm': 'nic_nes', 'nb_offspring': P,
+                             'config': {'noise_stdev': 0.01, 'batch_size': 8, 'l2coeff': 1e-3, 'snapshot_freq': 0,
+                                        'single_batch': True},
+                             'policy_options': {'net': 'fc_caption', 'fitness': 'greedy',
+                                                'model_options': {'safe_mutations': 'SM-G-SUM',
+                                                                  'safe_mutation_underflow': 0.1}},
+                             'optimizer_options': {'type': 'adam', 'args': {'stepsize': 1e-3}}})
+    e = nicnes.Engine(max_batch=8, max_members=P, noise_len=NOISE_LEN, noise_seed=0)
+    try:
+        e.set_noise_table(table)
+        keys, vals = nicnes.df_table_arrays(df)
+        e.set_df_table(keys, vals, np.log(float(n)))
+        batch = {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts}
+        gpu = M.EngineMaster(spec, e, theta=theta)
+        gpu.run([batch], max_iterations=2)
+        ora_e = OracleEngine(dims, theta, fc, gts, df, n, table, noise_seed=0)
+        ora = M.EngineMaster(spec, ora_e, theta=theta)
+        ora.run([batch], max_iterations=2)
+        assert e.mutation_mode == 1 and np.array_equal(gpu.mutator.vector.numpy(), ora.mutator.vector.numpy())
+        for a, b in zip(gpu.stats, ora.stats):
+            assert abs(a['score_mean'] - b['score_mean']) <= 1e-9 * max(1.0, abs(b['score_mean']))
+        assert np.allclose(e.theta()[0].cpu().numpy(), ora_e.adam.theta, rtol=1e-6, atol=1e-12)
+    finally:
+        e.close()
