@@ -47,11 +47,10 @@ NN_FN float nn_pow2i(int32_t n) { return nn_i2f((n + 127) << 23); }
  * above 88.72 the result is +inf and NaN passes through. Branch-free (one instruction stream for
  * every lane of a wavefront).
  */
-NN_FN float nn_expf(float x) {
+NN_FN float nn_expf_core(float xc) {                   /* xc in [-87, 88], not NaN */
     const float log2e = 1.44269502162933349609375f;
     const float ln2_hi = 0.693145751953125f;          /* 12 significant bits: n*ln2_hi exact */
     const float ln2_lo = 1.428606765330187045e-06f;
-    const float xc = fminf(fmaxf(x, -87.0f), 88.0f);  /* NaN -> -87 (replaced below) */
     float n = nn_floorf(xc * log2e + 0.5f);
     float r = fmaf(-n, ln2_hi, xc);
     r = fmaf(-n, ln2_lo, r);
@@ -63,7 +62,12 @@ NN_FN float nn_expf(float x) {
     p = fmaf(p, r, 0.5f);
     p = fmaf(p, r, 1.0f);
     p = fmaf(p, r, 1.0f);
-    float y = p * nn_pow2i((int32_t)n);               /* n in [-126, 127] */
+    return p * nn_pow2i((int32_t)n);                  /* n in [-126, 127] */
+}
+
+NN_FN float nn_expf(float x) {
+    const float xc = fminf(fmaxf(x, -87.0f), 88.0f);  /* NaN -> -87 (replaced below) */
+    float y = nn_expf_core(xc);
     y = x > 88.72283935546875f ? nn_i2f(0x7f800000) : y;
     return x != x ? x : y;
 }
@@ -87,8 +91,8 @@ NN_FN float nn_rcp1f(float d) {
  * clamped to [-80, 80] (sigmoid there is 1 - 2^-115 .. 2^-115 off its limit) so 1 + e^-x stays in the
  * reciprocal's range */
 NN_FN float nn_sigmoidf(float x) {
-    const float xc = fminf(fmaxf(x, -80.0f), 80.0f);
-    const float y = nn_rcp1f(1.0f + nn_expf(-xc));
+    const float xc = fminf(fmaxf(x, -80.0f), 80.0f);   /* NaN -> -80 (replaced below) */
+    const float y = nn_rcp1f(1.0f + nn_expf_core(-xc)); /* = nn_expf(-xc): -xc is in range */
     return x != x ? x : y;
 }
 
@@ -108,9 +112,9 @@ NN_FN float nn_tanhf(float x) {
     p = fmaf(p, u, -0.3333333134651184f);
     p = fmaf(p, u, 1.0f);
     const float small = x * p;
-    const float ac = a > 9.5f ? 9.5f : a;             /* e^19 + 1 < 2^28: in the reciprocal's range */
-    float y = 1.0f - 2.0f * nn_rcp1f(nn_expf(2.0f * ac) + 1.0f);
-    y = a > 9.5f ? 1.0f : y;
+    const float ac = fminf(a, 9.5f);                  /* e^19 + 1 < 2^28: in the reciprocal's range; */
+    float y = 1.0f - 2.0f * nn_rcp1f(nn_expf_core(2.0f * ac) + 1.0f);   /* NaN -> 9.5, replaced below */
+    /* past 9.5 the formula already gives exactly 1: 2 / (e^19 + 1) < ulp(1) / 2 below 1 */
     y = x < 0.0f ? -y : y;
     y = a < 0.6f ? small : y;
     return x != x ? x : y;

@@ -44,7 +44,7 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #define NEG_INF (-__builtin_inff())
 
 #ifndef DECODE_ABLATE
-#define DECODE_ABLATE 0    // timing-only builds (scripts/ablate.py): 1 no logit epilogue, 2 no stage
+#define DECODE_ABLATE 0    // timing-only builds (scripts/ablate.py): 1 no logit epilogue, 4 no exp-sum, 2 no stage
 #endif                     // staging, 8 no stage-loop barrier, 16 no cell activations, 64 no early
                            // exit -- wrong results
 #if DECODE_ABLATE & 16
@@ -54,6 +54,19 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #define CELL_SIG(x) nn_sigmoidf(x)
 #define CELL_TANH(x) nn_tanhf(x)
 #endif
+#ifndef CELL_PIPE
+#define CELL_PIPE 0        // fused cell: fold of stage m - 1 overlapped with the MFMAs of stage m
+#endif
+#ifndef DECODE_PRIO
+#define DECODE_PRIO 0      // s_setprio 1 for one half of the workgroup's waves: 1 = waves 4-7, 2 = waves 0-3
+#endif
+__device__ __forceinline__ void wave_prio(int wave) {
+#if DECODE_PRIO == 1
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#elif DECODE_PRIO == 2
+    if (wave < 4) __builtin_amdgcn_s_setprio(1);
+#endif
+}
 #ifndef DECODE_PROF
 #define DECODE_PROF 0      // timing-only build: per-workgroup start/end s_memrealtime (100 MHz) of every
 #endif                     // launch written over seq[wg * 4096 + slot] (wrong tokens; scripts/ablate.py)
@@ -477,8 +490,12 @@ __device__ __forceinline__ void epilogue64(RowState& st, const f32x16& P0, const
     const float mnew = vmax2(st.m, tmax);
     const float ml = mnew * LOG2E;
     float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
+#if !(DECODE_ABLATE & 4)
     expsum16(s, P0, ml);
     expsum16(s, P1, ml);
+#else
+    s += 64.0f;
+#endif
     st.s = s;
     st.m = mnew;
 }
@@ -749,6 +766,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const Ctx c = make_ctx(p);
     if (t > 0 && p.alive[c.wg] == 0) return;
+    wave_prio(c.wave);
     PROF_MARK(2 * (t + 1));
     const uint32_t lo = 4u * c.lane;
     const int nst = (p.V1 + 63) >> 6;
@@ -903,6 +921,40 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         for (int r = 0; r < 16; ++r) cp[r] = (m % 5 == 3 && t >= 0) ? ld1(c.scr_r, lo_, C_SLOT(16 * (m / 5) + r)) : 0.f;
         return cp;
     };
+#if CELL_PIPE
+    // software-pipelined: stage m's MFMA chains and the fold of stage m - 1 (the other accumulator
+    // set) run in opposite orders in the two waves of a SIMD (w, w + 4: opposite signs), so no wave
+    // waits for its own chains to drain before folding and the folds of a SIMD do not coincide
+    auto mfma_m = [&](int m, f32x16& x0, f32x16& x1) {
+        const float* buf = lds + ((m + b0) & 1) * STAGE64_FLOATS;
+        if (t < 0)      // h = 0 before the first cell: h2h(h) is its bias (fma(w, 0, acc) == acc)
+            mfma_xh_part<0, 4, false>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), x0, x1);
+        else
+            mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), x0, x1);
+    };
+    f32x16 A0, A1, B0, B1, cA, cB;
+    auto cstep = [&](int m, f32x16& x0, f32x16& x1, f32x16& cx, const f32x16& y0, const f32x16& y1,
+                     const f32x16& cy) {
+        cx = load_c(m);                                          // before the staging loads (in-order vmcnt)
+        __builtin_amdgcn_sched_barrier(0);
+        if (m < 19) stage64_load(csrc(m + 1), c.wave * 64 + lane_fresh(), s64);
+        if (c.sgn == 0) {
+            mfma_m(m, x0, x1);
+            if (m > 0) fold(m - 1, y0 + y1, cy);                 // i2h(x) + h2h(h), nets.py:109-111
+        } else {
+            if (m > 0) fold(m - 1, y0 + y1, cy);
+            mfma_m(m, x0, x1);
+        }
+        if (m < 19) stage64_store(lds + ((m + 1 + b0) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
+        __syncthreads();
+    };
+#pragma unroll 1
+    for (int m = 0; m < 20; m += 2) {
+        cstep(m, A0, A1, cA, B0, B1, cB);
+        cstep(m + 1, B0, B1, cB, A0, A1, cA);
+    }
+    fold(19, B0 + B1, cB);
+#else
 #pragma unroll 1
     for (int m = 0; m < 20; ++m) {
         const f32x16 cpre = load_c(m);                           // before the staging loads (in-order vmcnt)
@@ -918,6 +970,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         if (m < 19) stage64_store(lds + ((m + 1 + b0) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
         __syncthreads();
     }
+#endif
     PROF_MARK(2 * (t + 1) + 1);
 }
 
