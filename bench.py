@@ -226,7 +226,7 @@ def main():
         kname, n_step = 'nicnes_decode_logit_kernel<%d>' % G, ph['logit_launches']
         step_ms = float(np.mean([q['logit_ms'] for q in phases])) / n_step
         step_flop = logit_flops_per_member(B) * P_local / n_step
-        alg_bytes = logit_noise_bytes_per_member() * P_local / n_step
+        alg_bytes = logit_noise_bytes_per_member() * P_local      # every member's logit noise, once per launch
     achieved = step_flop / (step_ms / 1e3) / 1e12
     # counter figures of the same kernel and workload from the committed rocprofv3 PMC profile
     # (a profile-derived constant: PMC passes cannot run inside the timed bench process)

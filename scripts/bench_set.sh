@@ -1,0 +1,16 @@
+#!/bin/bash
+# The round's bench lines on one GPU (each step under its own time limit):
+#   default (bench.py with no flags: P = 512, B = 128, CPU baseline leg included),
+#   P = 64 (split decode), B = 64 at P = 512 and P = 64 (64-row slabs), 'bu' features, greedy_linprob.
+# usage (on the GPU box): bash scripts/bench_set.sh TAG
+set -eo pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:-benchset}
+mkdir -p $O
+timeout -k 10 400 python3 -u bench.py > $O/bench_default.json 2> $O/bench_default.err
+timeout -k 10 200 python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --pop-per-gpu 64 > $O/bench_p64.json 2> $O/bench_p64.err
+timeout -k 10 200 python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --batch 64 > $O/bench_b64.json 2> $O/bench_b64.err
+timeout -k 10 200 python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --pop-per-gpu 64 --batch 64 > $O/bench_p64_b64.json 2> $O/bench_p64_b64.err
+timeout -k 10 200 python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --bu > $O/bench_bu.json 2> $O/bench_bu.err
+timeout -k 10 200 python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --fitness greedy_linprob > $O/bench_linprob.json 2> $O/bench_linprob.err
+echo done

@@ -37,7 +37,7 @@ for P, key, kernel in ((512, 'step', 'nicnes_decode_step_kernel'), (64, 'logit',
         alg = bench.step_noise_bytes_per_member(B) * P / n_launch
     else:
         flop = bench.logit_flops_per_member(B) * P / 16
-        alg = bench.logit_noise_bytes_per_member() * P / 16
+        alg = bench.logit_noise_bytes_per_member() * P          # once per launch per member
     passes = []
     for i in range(4):
         passes += ['--pass', os.path.join(src, 'pmc%d_%d' % (P, i))]
