@@ -106,11 +106,13 @@ int nicnes_noise_vectors(nicnes_handle* h, uint64_t iteration, int32_t member_be
 
 /* Safe / proportional mutations (PolicyNet.evolve, src/algorithm/nets.py:96-113; Mutation enum :16-21):
  * the member's noise becomes delta' = fp32(fp32(sigma * z) / vec) with mode NICNES_MUTATION_DIVIDE
- * (SM-G-SUM, SM-G-ABS: vec = the sensitivity of src/algorithm/safe_mutations.py:93-147 after its
- * underflow clamp and scaling; SM-VECTOR: the loaded vector, :25-29) or fp32(fp32(sigma * z) * vec)
- * with NICNES_MUTATION_SCALE (SM-PROPORTIONAL: vec = |theta|, zeros replaced by mean |theta|).
- * vec [D] fp32 device (copied). Every later evaluate / grad_partial / noise_vectors uses delta'
- * (materialised per member, [max_members, D] on the device). NICNES_MUTATION_PLAIN turns it off. */
+ * (SM-G-SUM: vec = the sensitivity of src/algorithm/safe_mutations.py:34-117 after its underflow
+ * clamp and scaling; SM-VECTOR: the loaded vector, :27-31) or fp32(fp32(sigma * z) * vec) with
+ * NICNES_MUTATION_SCALE (SM-PROPORTIONAL: vec = |theta|, zeros replaced by mean |theta|).
+ * vec [D] fp32 device (copied). Every later evaluate / grad_partial / noise_vectors uses delta':
+ * an evaluation materialises it per member ([max_members, D] on the device, allocated at the first
+ * mutated evaluation), the weighted noise sum transforms each delta on the fly.
+ * NICNES_MUTATION_PLAIN turns it off. */
 #define NICNES_MUTATION_PLAIN 0
 #define NICNES_MUTATION_DIVIDE 1
 #define NICNES_MUTATION_SCALE 2
