@@ -481,7 +481,34 @@ __device__ __forceinline__ void expsum16(float& s, const f32x16& P, float ml) {
 // epilogue of one logit stage: P0 holds vocab vbase + (r&3) + 8(r>>2), P1 the same + 32.
 // Per stage and lane: 15 v_max3/v_max for the stage max, then 3 VALU per logit for the exp-sum; the
 // record scans run only in stages that raise some lane's running max (few once it settles).
+// PAIRS (greedy-only decodes, no log-prob output): the exp-sum runs over the maxima of adjacent
+// pairs, a lower bound s of the row's sum with the true sum in [s, 2s]; that fixes lse to within
+// ln 2, which is all the tie window needs except near a binade edge (tie_window / win_state).
+template <bool PAIRS>
 __device__ __forceinline__ void epilogue64(RowState& st, const f32x16& P0, const f32x16& P1, int vbase) {
+    if constexpr (PAIRS) {
+        float q[16];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            q[r] = vmax2(P0[2 * r], P0[2 * r + 1]);
+            q[8 + r] = vmax2(P1[2 * r], P1[2 * r + 1]);
+        }
+        const float a0 = vmax3(q[0], q[1], q[2]), a1 = vmax3(q[3], q[4], q[5]), a2 = vmax3(q[6], q[7], q[8]);
+        const float a3 = vmax3(q[9], q[10], q[11]), a4 = vmax3(q[12], q[13], q[14]);
+        const float tmax = vmax3(vmax3(a0, a1, a2), a3, vmax2(a4, q[15]));
+        if (__any(tmax > st.r1v)) {
+            records_scan(st, P0, vbase);
+            records_scan(st, P1, vbase + 32);
+        }
+        const float mnew = vmax2(st.m, tmax);
+        const float ml = mnew * LOG2E;
+        float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(q[r], LOG2E, -ml));
+        st.s = s;
+        st.m = mnew;
+        return;
+    }
     const float tmax = vmax2(vmax16(P0), vmax16(P1));
     if (__any(tmax > st.r1v)) {
         records_scan(st, P0, vbase);
@@ -512,8 +539,98 @@ __device__ __forceinline__ void logit_epilogue_exact(int& best, const f32x16& ac
 
 __device__ __forceinline__ bool in_window(float v, float m, float lse) { return ((v - m) - lse) == -lse; }
 
+// Tie window from a merged row state (m, s). Exact mode: lse = log(s) and in_window. PAIRS mode: s
+// bounds the sum within a factor 2, so lse lies in [log s, log s + ln 2] (widened by 2e-3 for the
+// fp32 sums and v_exp_f32). The window test fp32(d - lse) == -lse (d = x - m <= 0, lse >= 0) holds
+// iff e = -d < ulp(lse) / 2, fails iff e > ulp(lse) / 2, and at e == ulp / 2 depends on lse's last
+// bit, which no fp32 sum order pins (the reference's own lse bits are torch's): that tie is taken as
+// in the window, as a candidate at exactly half an ulp is by round-half-even for an even lse. With
+// hu_in / hu_out the half-ulps of the lowest / highest binade lse can be in, e <= hu_in is in,
+// e > hu_out is out; between them (lse's binade is not fixed by the bounds) the row goes to the exact pass.
+struct TieWindow {
+    float lse, hu_in, hu_out;
+    bool pairs;
+};
+
+__device__ __forceinline__ float binade_half_ulp(float a) {       // a > 0: 2^(E - 24) for a in [2^E, 2^(E+1))
+    const uint32_t ex = __builtin_bit_cast(uint32_t, a) >> 23;
+    return ex > 24u ? __builtin_bit_cast(float, (ex - 24u) << 23) : 0.f;
+}
+
+__device__ __forceinline__ TieWindow tie_window(float s, bool pairs) {
+    TieWindow w;
+    w.pairs = pairs;
+    w.lse = logf(s);
+    w.hu_in = w.hu_out = 0.f;
+    if (pairs) {
+        const float lo = w.lse - 2e-3f, hi = w.lse + (0.69314718f + 2e-3f);
+        w.hu_in = lo > 0.f ? binade_half_ulp(lo) : 0.f;
+        w.hu_out = binade_half_ulp(hi);
+    }
+    return w;
+}
+
+// 1 in the window, 0 out, 2 undecided (PAIRS mode only)
+__device__ __forceinline__ int win_state(float v, float m, const TieWindow& w) {
+    if (!w.pairs) return in_window(v, m, w.lse) ? 1 : 0;
+    const float e = m - v;
+    if (e == 0.f || e <= w.hu_in) return 1;
+    if (!(e <= w.hu_out)) return 0;                 // also NaN and unset (-inf) records
+    return 2;
+}
+
+// One sweep of the exact fallback over the whole vocabulary in 32-row tiles: sum mode accumulates the
+// row's exp-sum relative to m (PAIRS mode has no usable lse), otherwise the first id in the window
+__device__ __forceinline__ void exact_sweep(float* lds, const DecodeParams& p, rsrc_t theta_r, rsrc_t noise_r,
+                                            float sigma, int tid, int sgn, int hh, int lane, const float (&hB)[64],
+                                            bool active, bool sum_mode, float m, float lse, float& s, int& best) {
+    const int nvt = (p.V1 + 31) >> 5;
+    auto desc = [&](int n) {
+        TileDesc d;
+        d.w_off = (uint32_t)p.off_log_w; d.ld = 128; d.row0 = 32 * n; d.nvalid = min(32, p.V1 - 32 * n); d.k0 = 0;
+        d.b_off = (uint32_t)p.off_log_b; d.pad_bias = NEG_INF;
+        return d;
+    };
+    const float ml = m * LOG2E;
+    StageRegs sr;
+    stage_load(theta_r, noise_r, desc(0), tid, sr);
+    stage_store(lds, desc(0), sigma, tid, sr);
+    __syncthreads();
+    for (int n = 0; n < nvt; ++n) {
+        if (n + 1 < nvt) stage_load(theta_r, noise_r, desc(n + 1), tid, sr);
+        const float* buf = lds + (n & 1) * STAGE_FLOATS;
+        if (active) {
+            const f32x16 acc = mfma_tile(bias_init(buf + 2 * SIGN_FLOATS + 32 * sgn, hh), buf + sgn * SIGN_FLOATS, hB, lane);
+            if (sum_mode) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[r], LOG2E, -ml));
+            } else {
+                logit_epilogue_exact(best, acc, 32 * n + 4 * hh, m, lse);
+            }
+        }
+        if (n + 1 < nvt) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), sigma, tid, sr);
+        __syncthreads();
+    }
+}
+
 // epilogue of one 32-row logit tile (G = 2: one tile per wave); P0 holds vocab vbase + (r&3) + 8(r>>2)
+template <bool PAIRS>
 __device__ __forceinline__ void epilogue32(RowState& st, const f32x16& P0, int vbase) {
+    if constexpr (PAIRS) {
+        float q[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) q[r] = vmax2(P0[2 * r], P0[2 * r + 1]);
+        const float tmax = vmax3(vmax3(q[0], q[1], q[2]), vmax3(q[3], q[4], q[5]), vmax2(q[6], q[7]));
+        if (__any(tmax > st.r1v)) records_scan(st, P0, vbase);
+        const float mnew = vmax2(st.m, tmax);
+        const float ml = mnew * LOG2E;
+        float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(q[r], LOG2E, -ml));
+        st.s = s;
+        st.m = mnew;
+        return;
+    }
     const float tmax = vmax16(P0);
     if (__any(tmax > st.r1v)) records_scan(st, P0, vbase);
     const float mnew = vmax2(st.m, tmax);
@@ -530,7 +647,7 @@ __device__ __forceinline__ void epilogue32(RowState& st, const f32x16& P0, int v
 // Stages alternate between two accumulator sets, so no stage copies its result for the next one's
 // epilogue; the two waves of a SIMD (w, w + 4: opposite signs) run MFMA and epilogue in opposite
 // orders. On return the last stage_store went to buffer (s1 - s0) & 1 (a redundant copy).
-template <int G>
+template <int G, bool PAIRS>
 __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, uint64_t nidx, int wave, int sgn,
                                              int hf, float sigma, const float (&hB)[64], int s0, int s1, RowState& st) {
     const rsrc_t lw_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
@@ -567,11 +684,11 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
             if (sgn == 0) {
                 mfma_stage64_o(wsg, bsg, hB, lo.arow, hh, o0, o1);
 #if !(DECODE_ABLATE & 1)
-                epilogue64(st, q0, q1, 64 * (s - 1) + vl);
+                epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
 #endif
             } else {
 #if !(DECODE_ABLATE & 1)
-                epilogue64(st, q0, q1, 64 * (s - 1) + vl);
+                epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
 #endif
                 mfma_stage64_o(wsg, bsg, hB, lo.arow, hh, o0, o1);
             }
@@ -580,9 +697,9 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
             const float* bb = bsg + 32 * hf;
             if (sgn == 0) {
                 o0 = mfma_tile_o(bias_init(bb, hh), w1, hB, lo.arow);
-                epilogue32(st, q0, 64 * (s - 1) + vl);
+                epilogue32<PAIRS>(st, q0, 64 * (s - 1) + vl);
             } else {
-                epilogue32(st, q0, 64 * (s - 1) + vl);
+                epilogue32<PAIRS>(st, q0, 64 * (s - 1) + vl);
                 o0 = mfma_tile_o(bias_init(bb, hh), w1, hB, lo.arow);
             }
         }
@@ -595,9 +712,9 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
     };
     auto last = [&](const f32x16& q0, const f32x16& q1, int s) {
         if constexpr (G == 4)
-            epilogue64(st, q0, q1, 64 * s + vl);
+            epilogue64<PAIRS>(st, q0, q1, 64 * s + vl);
         else
-            epilogue32(st, q0, 64 * s + vl);
+            epilogue32<PAIRS>(st, q0, 64 * s + vl);
     };
     for (int s = s0; s < s1; s += 2) {
         stage(s, a0, a1, b0, b1);
@@ -762,6 +879,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
 // go to lane scratch. In the logit loop the two waves sharing a SIMD (w and w+4: opposite signs)
 // run the MFMA chains and the VALU epilogue of the previous stage in opposite orders, so VALU of
 // one wave overlaps the MFMAs of the other.
+template <bool PAIRS>
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodeParams p, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const Ctx c = make_ctx(p);
@@ -787,45 +905,42 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
     if (nl > 0) {
         RowState st;
         row_state_init(st);
-        logit_stages<4>(lds, p, nidx, c.wave, c.sgn, 0, c.sigma, hB, 0, nl, st);
+        logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, c.sigma, hB, 0, nl, st);
 
         // ---- greedy token (nets.py:208-209) ------------------------------------------------
         const float m_o = __shfl_xor(st.m, 32);
         const float s_o = __shfl_xor(st.s, 32);
         const float m = fmaxf(st.m, m_o);
         const float stot = st.s * __builtin_amdgcn_exp2f((st.m - m) * LOG2E) + s_o * __builtin_amdgcn_exp2f((m_o - m) * LOG2E);
-        const float lse = logf(stot);
+        const TieWindow w = tie_window(stot, PAIRS);
+        float lse = w.lse;
         int tok = 0x7fffffff;
+        bool amb = false;
         {
             const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
             const int ci[4] = {st.r0i, st.r1i, __shfl_xor(st.r0i, 32), __shfl_xor(st.r1i, 32)};
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (in_window(cv[k], m, lse) && ci[k] < tok) tok = ci[k];
-        }
-        const bool ovf = p.force_exact || in_window(st.ev, m, lse) || in_window(__shfl_xor(st.ev, 32), m, lse);
-        if (__syncthreads_or(ovf ? 1 : 0)) {
-            // rare: more records than tracked fall in the tie window -> exact second pass
-            const int nvt = (p.V1 + 31) >> 5;
-            auto desc = [&](int n) {
-                TileDesc d;
-                d.w_off = (uint32_t)p.off_log_w; d.ld = 128; d.row0 = 32 * n; d.nvalid = min(32, p.V1 - 32 * n); d.k0 = 0;
-                d.b_off = (uint32_t)p.off_log_b; d.pad_bias = NEG_INF;
-                return d;
-            };
-            StageRegs sr;
-            int best = 0x7fffffff;
-            stage_load(c.theta_r, c.noise_r, desc(0), c.tid, sr);
-            stage_store(lds, desc(0), c.sigma, c.tid, sr);
-            __syncthreads();
-            for (int n = 0; n < nvt; ++n) {
-                if (n + 1 < nvt) stage_load(c.theta_r, c.noise_r, desc(n + 1), c.tid, sr);
-                const float* buf = lds + (n & 1) * STAGE_FLOATS;
-                const f32x16 acc = mfma_tile(bias_init(buf + 2 * SIGN_FLOATS + 32 * c.sgn, c.hh), buf + c.sgn * SIGN_FLOATS, hB, c.lane);
-                if (n + 1 < nvt) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), c.sigma, c.tid, sr);
-                logit_epilogue_exact(best, acc, 32 * n + 4 * c.hh, m, lse);
-                __syncthreads();
+            for (int k = 0; k < 4; ++k) {
+                const int ws = win_state(cv[k], m, w);
+                if (ws == 1 && ci[k] < tok) tok = ci[k];
+                amb = amb || ws == 2;
             }
+        }
+        const bool ovf = p.force_exact || amb || win_state(st.ev, m, w) != 0 ||
+                         win_state(__shfl_xor(st.ev, 32), m, w) != 0;
+        if (__syncthreads_or(ovf ? 1 : 0)) {
+            // rare: more records than tracked fall in the tie window (or, PAIRS mode, the bounds on
+            // lse leave a record undecided) -> exact pass: the exp-sum first if PAIRS, then the first
+            // id in the window
+            int best = 0x7fffffff;
+            float ssum = 0.f;
+            if (PAIRS) {
+                exact_sweep(lds, p, c.theta_r, c.noise_r, c.sigma, c.tid, c.sgn, c.hh, c.lane, hB, true, true, m, 0.f,
+                            ssum, best);
+                lse = logf(ssum + __shfl_xor(ssum, 32));
+            }
+            exact_sweep(lds, p, c.theta_r, c.noise_r, c.sigma, c.tid, c.sgn, c.hh, c.lane, hB, true, false, m, lse,
+                        ssum, best);
             tok = min(best, __shfl_xor(best, 32));
             if (c.tid == 0) atomicAdd(p.stats + 0, 1);
         }
@@ -995,7 +1110,7 @@ __device__ __forceinline__ float* part_ptr(const DecodeParams& p, int wg, int q,
     return p.part + (((size_t)wg * p.S + q) * 8 + wave) * (7 * 64);
 }
 
-template <int G>
+template <int G, bool PAIRS>
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_logit_kernel(DecodeParams p, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SCtx<G> c = make_sctx<G>(p);
@@ -1011,7 +1126,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_logit_kernel(DecodePar
     for (int i = 0; i < 64; ++i) pin(hB[i]);
     RowState st;
     row_state_init(st);
-    if (s1 > s0) logit_stages<G>(lds, p, nidx, c.wave, c.sgn, c.hf, c.sigma, hB, s0, s1, st);
+    if (s1 > s0) logit_stages<G, PAIRS>(lds, p, nidx, c.wave, c.sgn, c.hf, c.sigma, hB, s0, s1, st);
     float* pb = part_ptr(p, c.wg, c.q, c.wave) + lane_fresh();
     pb[0] = st.m;
     pb[64] = st.s;
@@ -1049,6 +1164,8 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
         float m = 0.f, lse = 0.f;
         int tok = 0x7fffffff;
         bool ovf = false;
+        const bool pairs = p.lp == nullptr;        // the logit kernel ran its PAIRS variant
+        TieWindow w = tie_window(1.f, false);
         if (folder) {
             const int nh = G == 4 ? 1 : 2;
             float mh = -1.0e30f, sh = 0.f;
@@ -1064,44 +1181,34 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
             const float s_o = __shfl_xor(sh, 32);
             m = fmaxf(mh, m_o);
             const float stot = sh * __builtin_amdgcn_exp2f((mh - m) * LOG2E) + s_o * __builtin_amdgcn_exp2f((m_o - m) * LOG2E);
-            lse = logf(stot);
+            w = tie_window(stot, pairs);
+            lse = w.lse;
             for (int q = 0; q < p.S; ++q)
                 for (int f = 0; f < nh; ++f) {
                     const float* pb = part_ptr(p, c.wg, q, c.wave + f) + c.lane;
                     const float r0v = pb[128], r1v = pb[256], ev = pb[384];
                     const int r0i = __builtin_bit_cast(int, pb[192]), r1i = __builtin_bit_cast(int, pb[320]);
-                    if (in_window(r0v, m, lse) && r0i < tok) tok = r0i;
-                    if (in_window(r1v, m, lse) && r1i < tok) tok = r1i;
-                    ovf = ovf || in_window(ev, m, lse);
+                    const int w0 = win_state(r0v, m, w), w1 = win_state(r1v, m, w);
+                    if (w0 == 1 && r0i < tok) tok = r0i;
+                    if (w1 == 1 && r1i < tok) tok = r1i;
+                    ovf = ovf || w0 == 2 || w1 == 2 || win_state(ev, m, w) != 0;
                 }
             tok = min(tok, __shfl_xor(tok, 32));
             ovf = ovf || (__shfl_xor(ovf ? 1 : 0, 32) != 0);
         }
         if (__syncthreads_or((p.force_exact || ovf) ? 1 : 0)) {
-            // rare: more records than tracked fall in the tie window -> exact second pass over the
-            // whole vocabulary (every workgroup of the member does it: it needs the token)
-            const int nvt = (p.V1 + 31) >> 5;
-            auto desc = [&](int n) {
-                TileDesc d;
-                d.w_off = (uint32_t)p.off_log_w; d.ld = 128; d.row0 = 32 * n; d.nvalid = min(32, p.V1 - 32 * n); d.k0 = 0;
-                d.b_off = (uint32_t)p.off_log_b; d.pad_bias = NEG_INF;
-                return d;
-            };
-            StageRegs sr;
+            // rare: more records than tracked fall in the tie window, or (PAIRS mode) the bounds on lse
+            // leave a record undecided -> exact pass over the whole vocabulary (every workgroup of the
+            // member does it: it needs the token); PAIRS mode sums the exp first
             int best = 0x7fffffff;
-            stage_load(c.theta_r, c.noise_r, desc(0), c.tid, sr);
-            stage_store(lds, desc(0), c.sigma, c.tid, sr);
-            __syncthreads();
-            for (int n = 0; n < nvt; ++n) {
-                if (n + 1 < nvt) stage_load(c.theta_r, c.noise_r, desc(n + 1), c.tid, sr);
-                const float* buf = lds + (n & 1) * STAGE_FLOATS;
-                if (folder) {
-                    const f32x16 acc = mfma_tile(bias_init(buf + 2 * SIGN_FLOATS + 32 * c.sgn, c.hh), buf + c.sgn * SIGN_FLOATS, hB, c.lane);
-                    logit_epilogue_exact(best, acc, 32 * n + 4 * c.hh, m, lse);
-                }
-                if (n + 1 < nvt) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), c.sigma, c.tid, sr);
-                __syncthreads();
+            float ssum = 0.f;
+            if (pairs) {
+                exact_sweep(lds, p, c.theta_r, c.noise_r, c.sigma, c.tid, c.sgn, c.hh, c.lane, hB, folder, true, m, 0.f,
+                            ssum, best);
+                lse = logf(ssum + __shfl_xor(ssum, 32));
             }
+            exact_sweep(lds, p, c.theta_r, c.noise_r, c.sigma, c.tid, c.sgn, c.hh, c.lane, hB, folder, false, m, lse,
+                        ssum, best);
             tok = min(best, __shfl_xor(best, 32));
             if (lead) atomicAdd(p.stats + 0, 1);
         }
@@ -1248,9 +1355,12 @@ const size_t LDS_CELL2 = LDS64 + (size_t)4 * 1024 * sizeof(float);   // + the G 
 // per device, once per handle (nicnes_create, after hipSetDevice): dynamic LDS above 64 KB
 extern "C" hipError_t nicnes_decode_init() {
     const struct { const void* f; size_t b; } ks[] = {
-        {(const void*)nicnes_decode_step_kernel, LDS64},
-        {(const void*)nicnes_decode_logit_kernel<4>, LDS64},
-        {(const void*)nicnes_decode_logit_kernel<2>, LDS64},
+        {(const void*)nicnes_decode_step_kernel<true>, LDS64},
+        {(const void*)nicnes_decode_step_kernel<false>, LDS64},
+        {(const void*)nicnes_decode_logit_kernel<4, true>, LDS64},
+        {(const void*)nicnes_decode_logit_kernel<4, false>, LDS64},
+        {(const void*)nicnes_decode_logit_kernel<2, true>, LDS64},
+        {(const void*)nicnes_decode_logit_kernel<2, false>, LDS64},
         {(const void*)nicnes_decode_cell_kernel<4>, LDS64},
         {(const void*)nicnes_decode_cell_kernel<2>, LDS_CELL2},
         {(const void*)nicnes_decode_img_kernel<4>, LDS32},
@@ -1278,13 +1388,19 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
         }
     };
     const dim3 block(NTHREADS);
+    // greedy-only decodes (no log-prob output) bound lse by pair maxima (PAIRS); with p->lp the exact
+    // exp-sum gives seq_logprobs
+    const bool pairs = p->lp == nullptr;
     mark(0);
     if (fused) {
         hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(1, member_count, nslabs), block, LDS32, stream, *p);
         mark(DK_IMG);
         const dim3 grid(member_count, nslabs);
         for (int t = -1; t <= p->T; ++t) {
-            hipLaunchKernelGGL(nicnes_decode_step_kernel, grid, block, LDS64, stream, *p, t);
+            if (pairs)
+                hipLaunchKernelGGL(nicnes_decode_step_kernel<true>, grid, block, LDS64, stream, *p, t);
+            else
+                hipLaunchKernelGGL(nicnes_decode_step_kernel<false>, grid, block, LDS64, stream, *p, t);
             mark(DK_STEP);
         }
     } else {
@@ -1295,7 +1411,10 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
             mark(DK_IMG);
             for (int t = -1; t <= p->T; ++t) {
                 if (t >= 1) {
-                    hipLaunchKernelGGL(nicnes_decode_logit_kernel<4>, gl, block, LDS64, stream, *p, t);
+                    if (pairs)
+                        hipLaunchKernelGGL((nicnes_decode_logit_kernel<4, true>), gl, block, LDS64, stream, *p, t);
+                    else
+                        hipLaunchKernelGGL((nicnes_decode_logit_kernel<4, false>), gl, block, LDS64, stream, *p, t);
                     mark(DK_LOGIT);
                 }
                 hipLaunchKernelGGL(nicnes_decode_cell_kernel<4>, gc, block, LDS64, stream, *p, t);
@@ -1306,7 +1425,10 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
             mark(DK_IMG);
             for (int t = -1; t <= p->T; ++t) {
                 if (t >= 1) {
-                    hipLaunchKernelGGL(nicnes_decode_logit_kernel<2>, gl, block, LDS64, stream, *p, t);
+                    if (pairs)
+                        hipLaunchKernelGGL((nicnes_decode_logit_kernel<2, true>), gl, block, LDS64, stream, *p, t);
+                    else
+                        hipLaunchKernelGGL((nicnes_decode_logit_kernel<2, false>), gl, block, LDS64, stream, *p, t);
                     mark(DK_LOGIT);
                 }
                 hipLaunchKernelGGL(nicnes_decode_cell_kernel<2>, gc, block, LDS_CELL2, stream, *p, t);
