@@ -1158,6 +1158,22 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
     }
 #pragma unroll
     for (int i = 0; i < 64; ++i) pin(hB[i]);
+    const uint32_t ib = (uint32_t)p.off_i2h_b, hb = (uint32_t)p.off_h2h_b, bmin = min(ib, hb);
+    auto csrc = [&](int m) {                                     // gate tile m: i2h rows | h2h rows
+        const uint32_t r = gate_row(m);
+        StageSrc Sx;
+        Sx.w_r = c.theta_r; Sx.z_r = c.noise_r; Sx.b_r = c.theta_r; Sx.bz_r = c.noise_r;
+        Sx.so_a = 4u * ((uint32_t)p.off_i2h_w + 128u * r);
+        Sx.so_b = 4u * ((uint32_t)p.off_h2h_w + 128u * r);
+        Sx.bso = 4u * (bmin + r);
+        Sx.bda = 4u * (ib - bmin); Sx.bdb = 4u * (hb - bmin);
+        Sx.valid = 64;
+        return Sx;
+    };
+    const int nb = 4 / (int)gridDim.x, m0 = 5 * nb * c.q, m1 = m0 + 5 * nb;
+    Stage64Regs s64;
+    // the first gate tile's rows do not depend on the token: their loads fly during the merge
+    if (t < p.T) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
     int it = 0;                                   // token fed to the next cell (0 = BOS at t = 0)
     if (t >= 1) {
         // ---- merge the S partial states of each row (lane halves combined last, as the fused kernel)
@@ -1167,32 +1183,50 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
         const bool pairs = p.lp == nullptr;        // the logit kernel ran its PAIRS variant
         TieWindow w = tie_window(1.f, false);
         if (folder) {
-            const int nh = G == 4 ? 1 : 2;
+            const int nh = G == 4 ? 1 : 2, nk = p.S * nh;     // partial k = q * nh + f, in (q, f) order
             float mh = -1.0e30f, sh = 0.f;
-            for (int q = 0; q < p.S; ++q)
-                for (int f = 0; f < nh; ++f) {
-                    const float* pb = part_ptr(p, c.wg, q, c.wave + f) + c.lane;
-                    const float mk = pb[0], sk = pb[64];
-                    const float mn = fmaxf(mh, mk);
-                    sh = sh * __builtin_amdgcn_exp2f((mh - mn) * LOG2E) + sk * __builtin_amdgcn_exp2f((mk - mn) * LOG2E);
-                    mh = mn;
+            for (int k0 = 0; k0 < nk; k0 += 8) {              // every load of 8 partials issued before use
+                float pm[8], ps[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int k = min(k0 + u, nk - 1);
+                    const float* pb = part_ptr(p, c.wg, k / nh, c.wave + k % nh) + c.lane;
+                    pm[u] = pb[0];
+                    ps[u] = pb[64];
                 }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (k0 + u < nk) {
+                        const float mn = fmaxf(mh, pm[u]);
+                        sh = sh * __builtin_amdgcn_exp2f((mh - mn) * LOG2E) + ps[u] * __builtin_amdgcn_exp2f((pm[u] - mn) * LOG2E);
+                        mh = mn;
+                    }
+            }
             const float m_o = __shfl_xor(mh, 32);
             const float s_o = __shfl_xor(sh, 32);
             m = fmaxf(mh, m_o);
             const float stot = sh * __builtin_amdgcn_exp2f((mh - m) * LOG2E) + s_o * __builtin_amdgcn_exp2f((m_o - m) * LOG2E);
             w = tie_window(stot, pairs);
             lse = w.lse;
-            for (int q = 0; q < p.S; ++q)
-                for (int f = 0; f < nh; ++f) {
-                    const float* pb = part_ptr(p, c.wg, q, c.wave + f) + c.lane;
-                    const float r0v = pb[128], r1v = pb[256], ev = pb[384];
-                    const int r0i = __builtin_bit_cast(int, pb[192]), r1i = __builtin_bit_cast(int, pb[320]);
-                    const int w0 = win_state(r0v, m, w), w1 = win_state(r1v, m, w);
-                    if (w0 == 1 && r0i < tok) tok = r0i;
-                    if (w1 == 1 && r1i < tok) tok = r1i;
-                    ovf = ovf || w0 == 2 || w1 == 2 || win_state(ev, m, w) != 0;
+            for (int k0 = 0; k0 < nk; k0 += 8) {
+                float r0v[8], r1v[8], ev[8];
+                int r0i[8], r1i[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int k = min(k0 + u, nk - 1);
+                    const float* pb = part_ptr(p, c.wg, k / nh, c.wave + k % nh) + c.lane;
+                    r0v[u] = pb[128]; r1v[u] = pb[256]; ev[u] = pb[384];
+                    r0i[u] = __builtin_bit_cast(int, pb[192]); r1i[u] = __builtin_bit_cast(int, pb[320]);
                 }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (k0 + u < nk) {
+                        const int w0 = win_state(r0v[u], m, w), w1 = win_state(r1v[u], m, w);
+                        if (w0 == 1 && r0i[u] < tok) tok = r0i[u];
+                        if (w1 == 1 && r1i[u] < tok) tok = r1i[u];
+                        ovf = ovf || w0 == 2 || w1 == 2 || win_state(ev[u], m, w) != 0;
+                    }
+            }
             tok = min(tok, __shfl_xor(tok, 32));
             ovf = ovf || (__shfl_xor(ovf ? 1 : 0, 32) != 0);
         }
@@ -1253,22 +1287,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
     }
 #pragma unroll
     for (int i = 0; i < 64; ++i) pin(xB[i]);
-    const uint32_t ib = (uint32_t)p.off_i2h_b, hb = (uint32_t)p.off_h2h_b, bmin = min(ib, hb);
-    auto csrc = [&](int m) {                                     // gate tile m: i2h rows | h2h rows
-        const uint32_t r = gate_row(m);
-        StageSrc Sx;
-        Sx.w_r = c.theta_r; Sx.z_r = c.noise_r; Sx.b_r = c.theta_r; Sx.bz_r = c.noise_r;
-        Sx.so_a = 4u * ((uint32_t)p.off_i2h_w + 128u * r);
-        Sx.so_b = 4u * ((uint32_t)p.off_h2h_w + 128u * r);
-        Sx.bso = 4u * (bmin + r);
-        Sx.bda = 4u * (ib - bmin); Sx.bdb = 4u * (hb - bmin);
-        Sx.valid = 64;
-        return Sx;
-    };
-    const int nb = 4 / (int)gridDim.x, m0 = 5 * nb * c.q, m1 = m0 + 5 * nb;
     const int hpar = (t + 1) & 1;
-    Stage64Regs s64;
-    stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
     stage64_store(lds, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
     __syncthreads();
     f32x16 hold;
