@@ -54,8 +54,8 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #define CELL_SIG(x) nn_sigmoidf(x)
 #define CELL_TANH(x) nn_tanhf(x)
 #endif
-#ifndef CELL_PIPE
-#define CELL_PIPE 0        // fused cell: fold of stage m - 1 overlapped with the MFMAs of stage m
+#ifndef MFMA_FIRST_SIGN
+#define MFMA_FIRST_SIGN 0  // logit stages: the sign whose waves run the stage's MFMAs before the previous epilogue
 #endif
 #ifndef DECODE_PRIO
 #define DECODE_PRIO 0      // s_setprio 1 for one half of the workgroup's waves: 1 = waves 4-7, 2 = waves 0-3
@@ -681,7 +681,7 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
         const float* wsg = buf + sgn * (64 * LDS_ROW);
         const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * sgn;
         if constexpr (G == 4) {
-            if (sgn == 0) {
+            if (sgn == MFMA_FIRST_SIGN) {
                 mfma_stage64_o(wsg, bsg, hB, lo.arow, hh, o0, o1);
 #if !(DECODE_ABLATE & 1)
                 epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
@@ -695,7 +695,7 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
         } else {
             const float* w1 = wsg + 32 * hf * LDS_ROW;         // this wave's 32-row tile of the stage
             const float* bb = bsg + 32 * hf;
-            if (sgn == 0) {
+            if (sgn == MFMA_FIRST_SIGN) {
                 o0 = mfma_tile_o(bias_init(bb, hh), w1, hB, lo.arow);
                 epilogue32<PAIRS>(st, q0, 64 * (s - 1) + vl);
             } else {
@@ -1036,40 +1036,6 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         for (int r = 0; r < 16; ++r) cp[r] = (m % 5 == 3 && t >= 0) ? ld1(c.scr_r, lo_, C_SLOT(16 * (m / 5) + r)) : 0.f;
         return cp;
     };
-#if CELL_PIPE
-    // software-pipelined: stage m's MFMA chains and the fold of stage m - 1 (the other accumulator
-    // set) run in opposite orders in the two waves of a SIMD (w, w + 4: opposite signs), so no wave
-    // waits for its own chains to drain before folding and the folds of a SIMD do not coincide
-    auto mfma_m = [&](int m, f32x16& x0, f32x16& x1) {
-        const float* buf = lds + ((m + b0) & 1) * STAGE64_FLOATS;
-        if (t < 0)      // h = 0 before the first cell: h2h(h) is its bias (fma(w, 0, acc) == acc)
-            mfma_xh_part<0, 4, false>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), x0, x1);
-        else
-            mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), x0, x1);
-    };
-    f32x16 A0, A1, B0, B1, cA, cB;
-    auto cstep = [&](int m, f32x16& x0, f32x16& x1, f32x16& cx, const f32x16& y0, const f32x16& y1,
-                     const f32x16& cy) {
-        cx = load_c(m);                                          // before the staging loads (in-order vmcnt)
-        __builtin_amdgcn_sched_barrier(0);
-        if (m < 19) stage64_load(csrc(m + 1), c.wave * 64 + lane_fresh(), s64);
-        if (c.sgn == 0) {
-            mfma_m(m, x0, x1);
-            if (m > 0) fold(m - 1, y0 + y1, cy);                 // i2h(x) + h2h(h), nets.py:109-111
-        } else {
-            if (m > 0) fold(m - 1, y0 + y1, cy);
-            mfma_m(m, x0, x1);
-        }
-        if (m < 19) stage64_store(lds + ((m + 1 + b0) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
-        __syncthreads();
-    };
-#pragma unroll 1
-    for (int m = 0; m < 20; m += 2) {
-        cstep(m, A0, A1, cA, B0, B1, cB);
-        cstep(m + 1, B0, B1, cB, A0, A1, cA);
-    }
-    fold(19, B0 + B1, cB);
-#else
 #pragma unroll 1
     for (int m = 0; m < 20; ++m) {
         const f32x16 cpre = load_c(m);                           // before the staging loads (in-order vmcnt)
@@ -1085,7 +1051,6 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         if (m < 19) stage64_store(lds + ((m + 1 + b0) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
         __syncthreads();
     }
-#endif
     PROF_MARK(2 * (t + 1) + 1);
 }
 
