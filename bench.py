@@ -136,6 +136,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--pop-per-gpu', type=int, default=512)
     ap.add_argument('--batch', type=int, default=128)
+    ap.add_argument('--batches', type=int, default=1, help='distinct batches per iteration (single_batch: false, '
+                    'member i on batch i mod N)')
     ap.add_argument('--sigma', type=float, default=0.01)
     ap.add_argument('--noise-len', type=int, default=1 << 27)
     ap.add_argument('--bu', action='store_true', help="'bu' features: ReLU(N(0,1)) fc (configs[4])")
@@ -178,14 +180,14 @@ def main():
     P = P_local * world
     eng = nicnes.Engine(max_batch=B, max_members=P_local, noise_len=args.noise_len, noise_seed=0,
                         device=dev)
-    S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu)
+    S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu, batches=args.batches)
     eng.set_fitness_mode(args.fitness)
     eng.set_decode_split(args.decode_split, args.decode_rows)
     runner = PopulationRunner(eng, P, args.sigma, l2coeff=1e-7, stepsize=1e-3, rank=rank, world_size=world,
                               group=group)
     it = 1
     for _ in range(args.warmup):
-        runner.step(it, sync=False)
+        runner.step(it, sync=False, n_batches=args.batches)
         it += 1
     eng.set_timing(True)
     dec_ms, phases = [], []
@@ -194,7 +196,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        runner.step(it, sync=False)          # enqueue only: no host round trip inside the loop
+        runner.step(it, sync=False, n_batches=args.batches)   # enqueue only (a batch map is one small copy)
         it += 1
     torch.cuda.synchronize()
     if world > 1:
@@ -242,8 +244,11 @@ def main():
         'config': {'workload': 'mscoco_nes.json fc_caption, pop=%d antithetic (%d/GPU), batch_size=%d unique '
                                'images, sigma %.3g, full iteration (decode+CIDEr-D+ranks+noise sum+Adam)'
                                % (P, P_local, B, args.sigma) + (", 'bu' fc features" if args.bu else '')
-                               + (', fitness %s' % args.fitness if args.fitness != 'greedy' else ''),
-                   'population': P, 'members_per_gpu': P_local, 'batch_size': B, 'seq_length': 16,
+                               + (', fitness %s' % args.fitness if args.fitness != 'greedy' else '')
+                               + (', %d batches per iteration (single_batch false: member i on batch i mod %d)'
+                                  % (args.batches, args.batches) if args.batches > 1 else ''),
+                   'population': P, 'members_per_gpu': P_local, 'batch_size': B, 'batches_per_iteration': args.batches,
+                   'seq_length': 16,
                    'vocab_size': 9487,
                    'parallelism': ('none (one GPU, no collective)' if world == 1 else
                                    'population-sharded x%d, %s all-gather of fitness + all-reduce of the noise sum'

@@ -71,11 +71,11 @@ class PopulationRunner:
         return self.e.adam_step(self.gsum, self.P, self.l2coeff, self.stepsize, self.beta1, self.beta2,
                                 self.epsilon, sync=sync)
 
-    def step(self, iteration, sync=True):
+    def step(self, iteration, sync=True, n_batches=1):
         """One full NES iteration. Returns (fitness [P, 2] on device, update ratio). With sync=False the
         iteration is only enqueued (ratio None): back-to-back iterations then keep the GPU busy, so
-        its clock does not drop between them."""
-        self.evaluate(iteration)
+        its clock does not drop between them. n_batches > 1: per-member batches (evaluate)."""
+        self.evaluate(iteration, n_batches)
         self.exchange_fitness()
         ratio = self.update(iteration, sync=sync)
         return self.fit_all, ratio

@@ -104,8 +104,10 @@ def build_references(base_captions, vocab_size, seed=4321, n_refs=5, df_sets=409
 
 
 def setup_engine_workload(engine, B=128, theta_seed=0, fc_seed=1234, bu=False, noise=None, ref_seed=4321,
-                          df_sets=4096):
+                          df_sets=4096, batches=1):
     """Load a full synthetic workload into an Engine: noise table, theta, fc, refs + df.
+    batches > 1: that many batches of B images each (per-member batches, single_batch: false), held
+    with set_batches; fc / gts / base then cover all batches * B images in batch order.
     Returns dict(theta32, fc, gts, df, ref_len_raw, base)."""
     dims = Dims(engine.cfg.vocab_size, engine.cfg.input_encoding_size, engine.cfg.rnn_size,
                 engine.cfg.fc_feat_size, engine.cfg.seq_length)
@@ -114,15 +116,22 @@ def setup_engine_workload(engine, B=128, theta_seed=0, fc_seed=1234, bu=False, n
     engine.set_noise_table(noise)
     theta = init_theta(dims, theta_seed)
     engine.set_theta(theta)
-    fc = fc_feats(B, dims.F, fc_seed, bu)
+    n = B * batches
+    fc = fc_feats(n, dims.F, fc_seed, bu)
     # the base-theta greedy captions seed the references: decode once with sigma = 0
     placeholder = [np.zeros((1, dims.T), np.int32) for _ in range(B)]
     engine.set_df_table(np.zeros(0, np.uint64), np.zeros(0), np.log(float(df_sets)))
-    engine.set_batch(fc, placeholder)
-    _, seq = engine.evaluate(0, 0, 1, 0.0, return_seq=True)
-    base = seq[0, 0].cpu().numpy()
+    bases = []
+    for g in range(batches):
+        engine.set_batch(fc[g * B:(g + 1) * B], placeholder)
+        _, seq = engine.evaluate(0, 0, 1, 0.0, return_seq=True)
+        bases.append(seq[0, 0].cpu().numpy())
+    base = np.concatenate(bases)
     gts, df, ref_len_raw = build_references(base, dims.vocab_size, ref_seed, 5, df_sets, dims.T)
     keys, vals = df_table_arrays(df)
     engine.set_df_table(keys, vals, np.log(float(ref_len_raw)))
-    engine.set_batch(fc, gts)
+    if batches == 1:
+        engine.set_batch(fc, gts)
+    else:
+        engine.set_batches([(fc[g * B:(g + 1) * B], gts[g * B:(g + 1) * B]) for g in range(batches)])
     return dict(theta32=theta, fc=fc, gts=gts, df=df, ref_len_raw=ref_len_raw, base=base, dims=dims)
