@@ -54,7 +54,9 @@ int nicnes_destroy(nicnes_handle* h);
 const char* nicnes_last_error(const nicnes_handle* h);
 
 /* Shared noise table (borrowed), replaces the per-worker torch.normal_ draw of
- * PolicyNet.evolve, src/algorithm/nets.py:101-102. */
+ * PolicyNet.evolve, src/algorithm/nets.py:101-102. The engine keeps a sigma-scaled copy
+ * fp32(sigma * table) for the decode (noise_len floats of device memory), rebuilt by the first
+ * evaluation after this call or after a change of sigma; call again if the table's contents change. */
 int nicnes_set_noise_table(nicnes_handle* h, const float* table, uint64_t len);
 
 /* Current parameters (copied into the engine's fp64 master + fp32 evaluation copy), replaces

@@ -7,7 +7,7 @@
 
 struct DecodeParams {
     const float* theta;          // base theta, fp32 [D] (flat order: SURVEY.md Appendix A.1)
-    const float* noise;          // shared Gaussian table, fp32 [noise_len]
+    const float* noise;          // the sigma-scaled table fp32(sigma * z) [noise_len], or a mutation's delta' rows
     const uint64_t* noise_idx;   // per member slice start (multiple of 64)
     const float* fc;             // unique-image fc features [images, F]
     const int32_t* member_batch; // nullable: member k of the launch decodes images member_batch[k] * B .. + B
@@ -18,7 +18,6 @@ struct DecodeParams {
     int32_t* alive;              // fused path: [members * slabs], 0 once every row of the workgroup finished
     int32_t* alive2;             // split path: [2][alive_stride] by step parity
     float* part;                 // split path: [members * slabs * S] x PART_FLOATS partial greedy states
-    float sigma;
     int32_t force_exact;         // test hook (NICNES_FORCE_EXACT=1): every step takes the exact tie pass
     int32_t B, F, V1, T;
     int32_t G;                   // row groups per slab: 4 (128-row slabs) or 2 (64-row slabs)

@@ -151,19 +151,19 @@ __device__ __forceinline__ void stage_load(rsrc_t theta_r, rsrc_t noise_r, const
     }
 }
 
-__device__ __forceinline__ void stage_store(float* buf, const TileDesc& d, float sigma, int tid, const StageRegs& s) {
+__device__ __forceinline__ void stage_store(float* buf, const TileDesc& d, int tid, const StageRegs& s) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         const int f = tid + NTHREADS * u, row = f >> 5, q = f & 31;
         const int T = q >> 3, hh = q & 1, a = (q & 7) >> 1;
         const int o = row * LDS_ROW + T * 32 + hh * 16 + 4 * a;
-        const f32x4 delta = sigma * s.z[u];           // fp32(sigma * z), nets.py:102
+        const f32x4 delta = s.z[u];                   // fp32(sigma * z) from the sigma-scaled table, nets.py:102
         *reinterpret_cast<f32x4*>(buf + o) = s.w[u] + delta;            // nets.py:113
         *reinterpret_cast<f32x4*>(buf + SIGN_FLOATS + o) = s.w[u] - delta;   // nic_nes_worker.py:151
     }
     {   // slot (tid & 63): bias+ rows 0..31, bias- rows 32..63 (every wave writes the same values)
         const int r = tid & 31;
-        const float delta = sigma * s.bz;
+        const float delta = s.bz;
         const float v = (tid & 32) ? s.bw - delta : s.bw + delta;
         buf[2 * SIGN_FLOATS + (tid & 63)] = r < d.nvalid ? v : d.pad_bias;
     }
@@ -247,18 +247,18 @@ __device__ __forceinline__ void stage64_load(const StageSrc& S, int tid, Stage64
     }
 }
 
-__device__ __forceinline__ void stage64_store(float* buf, int valid, float sigma, int tid, const Stage64Regs& r) {
+__device__ __forceinline__ void stage64_store(float* buf, int valid, int tid, const Stage64Regs& r) {
     // thread tid writes rows (tid >> 5) + 16u: one base offset, the row step rides in the ds offset
     const int q = tid & 31;
     float* b = buf + (tid >> 5) * LDS_ROW + (q >> 3) * 32 + (q & 1) * 16 + 4 * ((q & 7) >> 1);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const f32x4 delta = sigma * r.z[u];           // fp32(sigma * z), nets.py:102
+        const f32x4 delta = r.z[u];                   // fp32(sigma * z) from the sigma-scaled table, nets.py:102
         *reinterpret_cast<f32x4*>(b + 16 * u * LDS_ROW) = r.w[u] + delta;                  // nets.py:113
         *reinterpret_cast<f32x4*>(b + (64 + 16 * u) * LDS_ROW) = r.w[u] - delta;           // nic_nes_worker.py:151
     }
     const int row = tid & 63, sg = (tid >> 6) & 1;     // every pair of waves writes all 128 slots
-    const float delta = sigma * r.bz;
+    const float delta = r.bz;
     const float v = sg ? r.bw - delta : r.bw + delta;
     buf[2 * 64 * LDS_ROW + 64 * sg + row] = row < valid ? v : NEG_INF;
 }
@@ -298,17 +298,17 @@ __device__ __forceinline__ void stage64_load_o(const StageSrc& S, const LaneOffs
     }
 }
 
-__device__ __forceinline__ void stage64_store_o(float* buf, int valid, float sigma, const LaneOffs& o, bool bias,
+__device__ __forceinline__ void stage64_store_o(float* buf, int valid, const LaneOffs& o, bool bias,
                                                 const Stage64Regs& r) {
     float* b = buf + o.so;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-        const f32x4 delta = sigma * r.z[u];           // fp32(sigma * z), nets.py:102
+        const f32x4 delta = r.z[u];                   // fp32(sigma * z) from the sigma-scaled table, nets.py:102
         *reinterpret_cast<f32x4*>(b + 16 * u * LDS_ROW) = r.w[u] + delta;                  // nets.py:113
         *reinterpret_cast<f32x4*>(b + (64 + 16 * u) * LDS_ROW) = r.w[u] - delta;           // nic_nes_worker.py:151
     }
     if (bias) {
-        const float delta = sigma * r.bz;
+        const float delta = r.bz;
         const float v = o.bslot >= 64 ? r.bw - delta : r.bw + delta;
         buf[2 * 64 * LDS_ROW + o.bslot] = (o.bslot & 63) < valid ? v : NEG_INF;
     }
@@ -582,7 +582,7 @@ __device__ __forceinline__ int win_state(float v, float m, const TieWindow& w) {
 // One sweep of the exact fallback over the whole vocabulary in 32-row tiles: sum mode accumulates the
 // row's exp-sum relative to m (PAIRS mode has no usable lse), otherwise the first id in the window
 __device__ __forceinline__ void exact_sweep(float* lds, const DecodeParams& p, rsrc_t theta_r, rsrc_t noise_r,
-                                            float sigma, int tid, int sgn, int hh, int lane, const float (&hB)[64],
+                                            int tid, int sgn, int hh, int lane, const float (&hB)[64],
                                             bool active, bool sum_mode, float m, float lse, float& s, int& best) {
     const int nvt = (p.V1 + 31) >> 5;
     auto desc = [&](int n) {
@@ -594,7 +594,7 @@ __device__ __forceinline__ void exact_sweep(float* lds, const DecodeParams& p, r
     const float ml = m * LOG2E;
     StageRegs sr;
     stage_load(theta_r, noise_r, desc(0), tid, sr);
-    stage_store(lds, desc(0), sigma, tid, sr);
+    stage_store(lds, desc(0), tid, sr);
     __syncthreads();
     for (int n = 0; n < nvt; ++n) {
         if (n + 1 < nvt) stage_load(theta_r, noise_r, desc(n + 1), tid, sr);
@@ -608,7 +608,7 @@ __device__ __forceinline__ void exact_sweep(float* lds, const DecodeParams& p, r
                 logit_epilogue_exact(best, acc, 32 * n + 4 * hh, m, lse);
             }
         }
-        if (n + 1 < nvt) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), sigma, tid, sr);
+        if (n + 1 < nvt) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), tid, sr);
         __syncthreads();
     }
 }
@@ -649,7 +649,7 @@ __device__ __forceinline__ void epilogue32(RowState& st, const f32x16& P0, int v
 // orders. On return the last stage_store went to buffer (s1 - s0) & 1 (a redundant copy).
 template <int G, bool PAIRS>
 __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, uint64_t nidx, int wave, int sgn,
-                                             int hf, float sigma, const float (&hB)[64], int s0, int s1, RowState& st) {
+                                             int hf, const float (&hB)[64], int s0, int s1, RowState& st) {
     const rsrc_t lw_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
     const rsrc_t lz_r = make_rsrc(p.noise + nidx + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
     const rsrc_t lbw_r = make_rsrc(p.theta + p.off_log_b, 4u * (uint32_t)p.V1);
@@ -667,7 +667,7 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
     const bool bias = wave < 2;
     Stage64Regs s64;
     stage64_load_o(lsrc(s0), lo, bias, s64);
-    stage64_store_o(lds, lsrc(s0).valid, sigma, lo, bias, s64);
+    stage64_store_o(lds, lsrc(s0).valid, lo, bias, s64);
     __syncthreads();
     f32x16 a0, a1, b0, b1;
 #pragma unroll
@@ -704,7 +704,7 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
             }
         }
 #if !(DECODE_ABLATE & 2)
-        stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, sigma, lo, bias, s64);
+        stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
 #endif
 #if !(DECODE_ABLATE & 8)
         __syncthreads();
@@ -743,7 +743,6 @@ __device__ __forceinline__ uint32_t gate_row(int m) { return (uint32_t)(tile_q(m
 struct Ctx {
     int tid, lane, wave, sgn, grp, hh, member, slab, b, bc, wg;
     bool row_valid;
-    float sigma;
     rsrc_t theta_r, noise_r, scr_r;
 };
 
@@ -761,7 +760,6 @@ __device__ __forceinline__ Ctx make_ctx(const DecodeParams& p) {
     c.b = c.slab * 128 + c.grp * 32 + (c.lane & 31);
     c.row_valid = c.b < p.B;
     c.bc = c.row_valid ? c.b : 0;
-    c.sigma = p.sigma;
     const uint64_t nidx = p.noise_idx[c.member];
     const uint32_t Dbytes = 4u * (uint32_t)p.D;
     c.theta_r = make_rsrc(p.theta, Dbytes);
@@ -780,7 +778,6 @@ template <int G>
 struct SCtx {
     int tid, lane, wave, sgn, grp, hf, hh, member, slab, q, wg, b, bc;
     bool row_valid;
-    float sigma;
     rsrc_t theta_r, noise_r, scr_r;
 };
 
@@ -801,7 +798,6 @@ __device__ __forceinline__ SCtx<G> make_sctx(const DecodeParams& p) {
     c.b = c.slab * (32 * G) + c.grp * 32 + (c.lane & 31);
     c.row_valid = c.b < p.B;
     c.bc = c.row_valid ? c.b : 0;
-    c.sigma = p.sigma;
     const uint64_t nidx = p.noise_idx[c.member];
     const uint32_t Dbytes = 4u * (uint32_t)p.D;
     c.theta_r = make_rsrc(p.theta, Dbytes);
@@ -836,7 +832,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
         return d;
     };
     stage_load(c.theta_r, c.noise_r, desc(0), c.tid, sr);
-    stage_store(lds, desc(0), c.sigma, c.tid, sr);
+    stage_store(lds, desc(0), c.tid, sr);
     __syncthreads();
     for (int kc = 0; kc < nK; ++kc) {
         const uint32_t frow = 4u * (uint32_t)(c.bc * p.F + 128 * kc + 4 * c.hh);
@@ -850,7 +846,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
                     if (kc == 0) accU[U] = bias_init(buf + 2 * SIGN_FLOATS + 32 * c.sgn, c.hh);
                     accU[U] = mfma_tile_fc(accU[U], buf + c.sgn * SIGN_FLOATS, fc_r, frow, c.lane);
                 }
-                if (n + 1 < ntile) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), c.sigma, c.tid, sr);
+                if (n + 1 < ntile) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), c.tid, sr);
                 __syncthreads();
             }
         }
@@ -905,7 +901,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
     if (nl > 0) {
         RowState st;
         row_state_init(st);
-        logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, c.sigma, hB, 0, nl, st);
+        logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st);
 
         // ---- greedy token (nets.py:208-209) ------------------------------------------------
         const float m_o = __shfl_xor(st.m, 32);
@@ -935,11 +931,11 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
             int best = 0x7fffffff;
             float ssum = 0.f;
             if (PAIRS) {
-                exact_sweep(lds, p, c.theta_r, c.noise_r, c.sigma, c.tid, c.sgn, c.hh, c.lane, hB, true, true, m, 0.f,
+                exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, true, true, m, 0.f,
                             ssum, best);
                 lse = logf(ssum + __shfl_xor(ssum, 32));
             }
-            exact_sweep(lds, p, c.theta_r, c.noise_r, c.sigma, c.tid, c.sgn, c.hh, c.lane, hB, true, false, m, lse,
+            exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, true, false, m, lse,
                         ssum, best);
             tok = min(best, __shfl_xor(best, 32));
             if (c.tid == 0) atomicAdd(p.stats + 0, 1);
@@ -978,7 +974,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
             for (int a = 0; a < 4; ++a) {
                 const f32x4 w = ld4(c.theta_r, eo + 4u * (32 * T + 8 * a));
                 const f32x4 z = ld4(c.noise_r, eo + 4u * (32 * T + 8 * a));
-                const f32x4 delta = c.sigma * z;
+                const f32x4 delta = z;                      // fp32(sigma * z): the table is sigma-scaled
                 const f32x4 x = c.sgn ? (w - delta) : (w + delta);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) xB[16 * T + 4 * a + e] = x[e];
@@ -1000,7 +996,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
     };
     const int b0 = nl & 1;                                       // next free stage buffer
     stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
-    stage64_store(lds + b0 * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
+    stage64_store(lds + b0 * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
     __syncthreads();
     f32x16 hold;
     // fold of gate tile m (s_ = its gate sums) into the unit block's c' / h'
@@ -1048,7 +1044,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         else
             mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
         fold(m, a0 + a1, cpre);                                  // i2h(x) + h2h(h), nets.py:109-111
-        if (m < 19) stage64_store(lds + ((m + 1 + b0) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
+        if (m < 19) stage64_store(lds + ((m + 1 + b0) & 1) * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
         __syncthreads();
     }
     PROF_MARK(2 * (t + 1) + 1);
@@ -1091,7 +1087,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_logit_kernel(DecodePar
     for (int i = 0; i < 64; ++i) pin(hB[i]);
     RowState st;
     row_state_init(st);
-    if (s1 > s0) logit_stages<G, PAIRS>(lds, p, nidx, c.wave, c.sgn, c.hf, c.sigma, hB, s0, s1, st);
+    if (s1 > s0) logit_stages<G, PAIRS>(lds, p, nidx, c.wave, c.sgn, c.hf, hB, s0, s1, st);
     float* pb = part_ptr(p, c.wg, c.q, c.wave) + lane_fresh();
     pb[0] = st.m;
     pb[64] = st.s;
@@ -1202,11 +1198,11 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
             int best = 0x7fffffff;
             float ssum = 0.f;
             if (pairs) {
-                exact_sweep(lds, p, c.theta_r, c.noise_r, c.sigma, c.tid, c.sgn, c.hh, c.lane, hB, folder, true, m, 0.f,
+                exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, folder, true, m, 0.f,
                             ssum, best);
                 lse = logf(ssum + __shfl_xor(ssum, 32));
             }
-            exact_sweep(lds, p, c.theta_r, c.noise_r, c.sigma, c.tid, c.sgn, c.hh, c.lane, hB, folder, false, m, lse,
+            exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, folder, false, m, lse,
                         ssum, best);
             tok = min(best, __shfl_xor(best, 32));
             if (lead) atomicAdd(p.stats + 0, 1);
@@ -1244,7 +1240,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
             for (int a = 0; a < 4; ++a) {
                 const f32x4 w = ld4(c.theta_r, eo + 4u * (32 * T + 8 * a));
                 const f32x4 z = ld4(c.noise_r, eo + 4u * (32 * T + 8 * a));
-                const f32x4 delta = c.sigma * z;
+                const f32x4 delta = z;                      // fp32(sigma * z): the table is sigma-scaled
                 const f32x4 x = c.sgn ? (w - delta) : (w + delta);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) xB[16 * T + 4 * a + e] = x[e];
@@ -1253,7 +1249,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
 #pragma unroll
     for (int i = 0; i < 64; ++i) pin(xB[i]);
     const int hpar = (t + 1) & 1;
-    stage64_store(lds, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
+    stage64_store(lds, 64, c.wave * 64 + lane_fresh(), s64);
     __syncthreads();
     f32x16 hold;
     auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) {
@@ -1302,7 +1298,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
             else
                 mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
             fold(m, a0 + a1, cpre);                              // i2h(x) + h2h(h), nets.py:109-111
-            if (m + 1 < m1) stage64_store(lds + ((m - m0 + 1) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
+            if (m + 1 < m1) stage64_store(lds + ((m - m0 + 1) & 1) * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
             __syncthreads();
         } else {
             // half 0: i2h tile over x (chain a); half 1: h2h tile over h (chain b), handed over in LDS
@@ -1324,7 +1320,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
                 for (int r = 0; r < 16; ++r) a1[r] = xch[r * 64 + l];
                 fold(m, a + a1, cpre);                           // i2h(x) + h2h(h), nets.py:109-111
             }
-            if (m + 1 < m1) stage64_store(lds + ((m - m0 + 1) & 1) * STAGE64_FLOATS, 64, c.sigma, c.wave * 64 + lane_fresh(), s64);
+            if (m + 1 < m1) stage64_store(lds + ((m - m0 + 1) & 1) * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
             __syncthreads();
         }
     }

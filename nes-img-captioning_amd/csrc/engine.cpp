@@ -78,6 +78,9 @@ struct nicnes_handle {
     int32_t* alive = nullptr;         // per decode workgroup: rows left unfinished (fused [stride], split [2][stride])
     int32_t alive_stride = 0;         // max decode workgroups (members x 64-row slabs)
     float* part = nullptr;            // split decode: partial greedy states
+    float* noise_sc = nullptr;        // fp32(sc_sigma * table): what the decode kernels read (no multiply per use)
+    float sc_sigma = 0.f;
+    bool sc_valid = false;
     int mut_mode = 0;                 // nicnes_set_mutation: 0 plain, 1 divide, 2 multiply
     float* mut_vec = nullptr;         // [D] sensitivity (mode 1) or |theta| scale (mode 2)
     float* dbuf = nullptr;            // [max_members, Dp] the members' mutated deltas (mode != 0)
@@ -335,7 +338,7 @@ int nicnes_destroy(nicnes_handle* h) {
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
                     h->ref_norm, h->nidx, h->seq, h->lp, h->row_scores, h->dscratch, h->stats, h->partials, h->norms,
                     h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive, h->part,
-                    h->rank_key, h->rank_idx, h->mbatch, h->mut_vec, h->dbuf, h->didx};
+                    h->rank_key, h->rank_idx, h->mbatch, h->mut_vec, h->dbuf, h->didx, h->noise_sc};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : h->ev)
@@ -354,6 +357,7 @@ int nicnes_set_noise_table(nicnes_handle* h, const float* table, uint64_t len) {
     if (((uintptr_t)table & 15u) != 0) return fail(h, NICNES_ERR_INVALID, "noise table must be 16-byte aligned");
     h->noise = table;
     h->noise_len = len;
+    h->sc_valid = false;          // the sigma-scaled copy is rebuilt at the next evaluation
     return NICNES_OK;
 }
 
@@ -603,11 +607,22 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
         if (rc) return rc;
         HIPC(h, nicnes_launch_iota_stride(h->didx, h->cfg.max_members, (uint64_t)h->Dp, s));
     }
-    if (h->mut_mode) {      // safe / proportional mutations: the decode reads the members' delta' with sigma 1
+    if (h->mut_mode) {      // safe / proportional mutations: the decode reads the members' delta' rows
         HIPC(h, nicnes_launch_mutate(h->noise, h->nidx, count, h->D, sigma, h->mut_vec, h->mut_mode, h->dbuf, h->Dp, s));
         p.noise = h->dbuf;
         p.noise_idx = h->didx;
-        sigma = 1.0f;
+    } else {                // the decode reads fp32(sigma * z) from the table scaled once per sigma
+        if (!h->noise_sc) {
+            HIPC(h, hipDeviceSynchronize());
+            int rc = dalloc(h, &h->noise_sc, (size_t)h->cfg.noise_len);
+            if (rc) return rc;
+        }
+        if (!h->sc_valid || __builtin_bit_cast(uint32_t, h->sc_sigma) != __builtin_bit_cast(uint32_t, sigma)) {
+            HIPC(h, nicnes_launch_scale(h->noise, h->noise_sc, h->cfg.noise_len, sigma, s));
+            h->sc_sigma = sigma;
+            h->sc_valid = true;
+        }
+        p.noise = h->noise_sc;
     }
     p.fc = h->fc;
     p.member_batch = mb;
@@ -616,7 +631,6 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     p.scratch = h->dscratch;
     p.stats = h->stats;
     p.alive = h->alive;
-    p.sigma = sigma;
     p.force_exact = h->force_exact;
     int G = 0, nslabs = 0, S = 0;
     decode_shape(h, h->B, count, &G, &nslabs, &S);

@@ -39,3 +39,5 @@ extern "C" hipError_t nicnes_launch_grad(const float* noise, const uint64_t* idx
                                          int64_t dim, const float* vec, int mode, float* gsum, hipStream_t s);
 extern "C" int nicnes_adam_blocks(int64_t dim);
 extern "C" hipError_t nicnes_launch_adam(const AdamParams* p, double* norms_out, hipStream_t s);
+// out[i] = fp32(sigma * in[i]), i < n (the decode's sigma-scaled noise table)
+extern "C" hipError_t nicnes_launch_scale(const float* in, float* out, uint64_t n, float sigma, hipStream_t s);

@@ -313,6 +313,23 @@ extern "C" hipError_t nicnes_launch_mutate(const float* noise, const uint64_t* i
     return hipGetLastError();
 }
 
+// the sigma-scaled table the decode kernels read: out[i] = fp32(sigma * table[i]), each member's
+// delta = fp32(sigma * z) (nets.py:102) then being a plain slice of it
+__global__ __launch_bounds__(256) void nicnes_scale_kernel(const float* in, float* out, uint64_t n, float sigma) {
+    const uint64_t n4 = n / 4;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
+        const f32x4 v = reinterpret_cast<const f32x4*>(in)[i];
+        reinterpret_cast<f32x4*>(out)[i] = sigma * v;
+    }
+    const uint64_t t = 4 * n4 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && t < n) out[t] = sigma * in[t];
+}
+
+extern "C" hipError_t nicnes_launch_scale(const float* in, float* out, uint64_t n, float sigma, hipStream_t s) {
+    hipLaunchKernelGGL(nicnes_scale_kernel, dim3(2048), dim3(256), 0, s, in, out, n, sigma);
+    return hipGetLastError();
+}
+
 __global__ void nicnes_iota_stride_kernel(uint64_t* out, int n, uint64_t stride) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = (uint64_t)i * stride;
