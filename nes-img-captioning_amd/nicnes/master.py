@@ -152,9 +152,14 @@ class EngineMaster:
             G = self.spec.batches_per_iteration
             while True:
                 if G == 1:
-                    yield batches.get_batch('train', batch_size=self.sched.batch_size)
+                    got = [batches.get_batch('train', batch_size=self.sched.batch_size)]
                 else:          # single_batch: false -- one batch per member (nic_nes_worker.py:121-128)
-                    yield [batches.get_batch('train', batch_size=self.sched.batch_size) for _ in range(G)]
+                    got = [batches.get_batch('train', batch_size=self.sched.batch_size) for _ in range(G)]
+                # a loader that wrapped around its split ends an epoch (the reference's outer loop,
+                # nic_nes_master.py:69-72, re-enters its train loader then)
+                if any(isinstance(b, dict) and b.get('bounds', {}).get('wrapped') for b in got):
+                    self.sched.epoch += 1
+                yield got[0] if G == 1 else got
         for b in batches:
             yield b
 
@@ -216,6 +221,7 @@ class EngineMaster:
         results whose task_id is not current (nic_nes_master.py:108-116)."""
         P = self.spec.nb_offspring
         client.declare_experiment(self.spec.exp)
+        self.sched.epoch += 1                   # it.incr_epoch() before the pass (nic_nes_master.py:70)
         done = 0
         for batch in self._batch_stream(batches):
             if done >= max_iterations:

@@ -452,3 +452,24 @@ def test_mutation_dispatched_loop_matches_local_loop(workload, tmp_path, mode):
     assert not th.is_alive()
     assert np.array_equal(local.e.theta()[0].numpy(), master.e.theta()[0].numpy())
     assert np.array_equal(e_worker.mutation[1], e_master.mutation[1])
+
+
+def test_epoch_counts_loader_wraps(workload):
+    """A loader batch with bounds['wrapped'] ends an epoch (the reference re-enters its train loader,
+    nic_nes_master.py:69-72); run_dispatched counts its own pass as one epoch."""
+    dims, theta, fc, gts, df, n, table = workload
+
+    class Wrapping:
+        def __init__(self):
+            self.k = 0
+
+        def get_batch(self, split, batch_size=None):
+            self.k += 1
+            return {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts, 'bounds': {'wrapped': self.k % 2 == 0}}
+    spec = C.ExperimentSpec(_exp(nb_offspring=4, config={'noise_stdev': 0.05, 'batch_size': 4, 'l2coeff': 1e-3,
+                                                         'snapshot_freq': 0, 'single_batch': True},
+                                 policy_options={'net': 'fc_caption', 'fitness': 'greedy'},
+                                 optimizer_options={'type': 'adam', 'args': {'stepsize': 0.01}}), vocab_size=63)
+    m = M.EngineMaster(spec, _engine(workload))
+    m.run(Wrapping(), max_iterations=4)
+    assert m.sched.epoch == 1 + 2            # the run's own pass + wraps after batches 2 and 4
