@@ -540,8 +540,8 @@ __device__ __forceinline__ void logit_epilogue_exact(int& best, const f32x16& ac
 __device__ __forceinline__ bool in_window(float v, float m, float lse) { return ((v - m) - lse) == -lse; }
 
 // Tie window from a merged row state (m, s). Exact mode: lse = log(s) and in_window. PAIRS mode: s
-// bounds the sum within a factor 2, so lse lies in [log s, log s + ln 2] (widened by 2e-3 for the
-// fp32 sums and v_exp_f32). The window test fp32(d - lse) == -lse (d = x - m <= 0, lse >= 0) holds
+// bounds the sum within a factor 2, so lse lies in [log s, log s + ln 2] (widened by p.lse_margin,
+// 2e-3, for the fp32 sums and v_exp_f32). The window test fp32(d - lse) == -lse (d = x - m <= 0, lse >= 0) holds
 // iff e = -d < ulp(lse) / 2, fails iff e > ulp(lse) / 2, and at e == ulp / 2 depends on lse's last
 // bit, which no fp32 sum order pins (the reference's own lse bits are torch's): that tie is taken as
 // in the window, as a candidate at exactly half an ulp is by round-half-even for an even lse. With
@@ -557,13 +557,13 @@ __device__ __forceinline__ float binade_half_ulp(float a) {       // a > 0: 2^(E
     return ex > 24u ? __builtin_bit_cast(float, (ex - 24u) << 23) : 0.f;
 }
 
-__device__ __forceinline__ TieWindow tie_window(float s, bool pairs) {
+__device__ __forceinline__ TieWindow tie_window(float s, bool pairs, float margin) {
     TieWindow w;
     w.pairs = pairs;
     w.lse = logf(s);
     w.hu_in = w.hu_out = 0.f;
     if (pairs) {
-        const float lo = w.lse - 2e-3f, hi = w.lse + (0.69314718f + 2e-3f);
+        const float lo = w.lse - margin, hi = w.lse + (0.69314718f + margin);
         w.hu_in = lo > 0.f ? binade_half_ulp(lo) : 0.f;
         w.hu_out = binade_half_ulp(hi);
     }
@@ -908,7 +908,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         const float s_o = __shfl_xor(st.s, 32);
         const float m = fmaxf(st.m, m_o);
         const float stot = st.s * __builtin_amdgcn_exp2f((st.m - m) * LOG2E) + s_o * __builtin_amdgcn_exp2f((m_o - m) * LOG2E);
-        const TieWindow w = tie_window(stot, PAIRS);
+        const TieWindow w = tie_window(stot, PAIRS, p.lse_margin);
         float lse = w.lse;
         int tok = 0x7fffffff;
         bool amb = false;
@@ -1142,7 +1142,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
         int tok = 0x7fffffff;
         bool ovf = false;
         const bool pairs = p.lp == nullptr;        // the logit kernel ran its PAIRS variant
-        TieWindow w = tie_window(1.f, false);
+        TieWindow w = tie_window(1.f, false, 0.f);
         if (folder) {
             const int nh = G == 4 ? 1 : 2, nk = p.S * nh;     // partial k = q * nh + f, in (q, f) order
             float mh = -1.0e30f, sh = 0.f;
@@ -1167,7 +1167,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
             const float s_o = __shfl_xor(sh, 32);
             m = fmaxf(mh, m_o);
             const float stot = sh * __builtin_amdgcn_exp2f((mh - m) * LOG2E) + s_o * __builtin_amdgcn_exp2f((m_o - m) * LOG2E);
-            w = tie_window(stot, pairs);
+            w = tie_window(stot, pairs, p.lse_margin);
             lse = w.lse;
             for (int k0 = 0; k0 < nk; k0 += 8) {
                 float r0v[8], r1v[8], ev[8];

@@ -101,6 +101,7 @@ struct nicnes_handle {
 
     bool timing = false;
     int force_exact = 0;      // test hook: exact tie pass on every step (NICNES_FORCE_EXACT=1)
+    float lse_margin = 2e-3f; // bounded-lse margin; test hook NICNES_LSE_MARGIN widens it (more undecided rows)
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     hipEvent_t dev[DECODE_MAX_EVENTS] = {};   // between the decode's launches (phase split)
     int dev_kind[DECODE_MAX_EVENTS] = {};     // kind of the launch each event follows (DK_*)
@@ -297,6 +298,8 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
     {
         const char* fe = getenv("NICNES_FORCE_EXACT");
         h->force_exact = (fe && fe[0] == '1') ? 1 : 0;
+        const char* lm = getenv("NICNES_LSE_MARGIN");
+        if (lm && lm[0]) h->lse_margin = (float)atof(lm);
     }
     {
         int ncu = 0;
@@ -632,6 +635,7 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     p.stats = h->stats;
     p.alive = h->alive;
     p.force_exact = h->force_exact;
+    p.lse_margin = h->lse_margin;
     int G = 0, nslabs = 0, S = 0;
     decode_shape(h, h->B, count, &G, &nslabs, &S);
     if ((int64_t)count * nslabs * S > h->part_cap)

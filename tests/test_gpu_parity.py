@@ -387,6 +387,33 @@ def test_exact_tie_pass_matches_oracle(monkeypatch):
         e.close()
 
 
+@pytest.mark.parametrize('shape', [(1, 4), (4, 2)], ids=['fused', 'split_G2S4'])
+def test_bounded_lse_undecided_rows_take_the_exact_pass(monkeypatch, shape):
+    """Greedy-only decodes bound lse from an exp-sum over pair maxima; a record whose window state the
+    bound leaves open goes to the exact pass. NICNES_LSE_MARGIN=1e5 widens the bound so that rows with
+    a record within ~0.004 of the max are undecided: the exact pass must run and the tokens still match the oracle."""
+    import nicnes
+    monkeypatch.setenv('NICNES_LSE_MARGIN', '1e5')
+    e = nicnes.Engine(max_batch=64, max_members=2, noise_len=NOISE_LEN, noise_seed=7)
+    try:
+        table = O.noise_table(NOISE_LEN, 123)
+        e.set_noise_table(table)
+        dims = O.Dims()
+        theta = O.make_theta(dims, 0, 1.0, 0.0)             # xavier: near-uniform logits, many near ties
+        fc = np.random.Generator(np.random.PCG64(99)).standard_normal((40, dims.F)).astype(np.float32)
+        _load(e, theta, fc)
+        e.set_decode_split(*shape)
+        _, seq = e.evaluate(3, 0, 2, SIGMA, return_seq=True)
+        seq = seq.cpu().numpy()
+        assert e.stats()['tie_fallbacks'] > 0
+        for k in range(2):
+            idx = int(e.noise_indices(3, k, 1).cpu().numpy()[0])
+            for s, (oseq, fr) in enumerate(_oracle_member(theta, table, idx, fc, dims)):
+                assert _compare_tokens(seq[k, s], oseq, fr) == 0
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize('P', [2048, 8192, 1000], ids=['P2048', 'P8192', 'P1000_partial_chunk'])
 def test_rank_weights_bit_exact_large(eng, P):
     """The sort-based rank (chunk bitonic sort + lower bounds) at configs[3]'s pop=2048 and beyond the
