@@ -902,6 +902,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         RowState st;
         row_state_init(st);
         logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st);
+        PROF_MARK(120 + 24 * (t + 1));
 
         // ---- greedy token (nets.py:208-209) ------------------------------------------------
         const float m_o = __shfl_xor(st.m, 32);
@@ -995,6 +996,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         return S;
     };
     const int b0 = nl & 1;                                       // next free stage buffer
+    PROF_MARK(120 + 24 * (t + 1) + 1);
     stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
     stage64_store(lds + b0 * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
     __syncthreads();
@@ -1046,6 +1048,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         fold(m, a0 + a1, cpre);                                  // i2h(x) + h2h(h), nets.py:109-111
         if (m < 19) stage64_store(lds + ((m + 1 + b0) & 1) * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
         __syncthreads();
+        PROF_MARK(120 + 24 * (t + 1) + 2 + m);
     }
     PROF_MARK(2 * (t + 1) + 1);
 }

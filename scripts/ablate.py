@@ -39,6 +39,30 @@ def launch_spans(k, seq):
         print('%-8s %9.1f %8.1f %8.1f %8.1f %8.1f %4d %8.1f %8.1f %6.3f %5.2f' % r)
 
 
+def cell_stages(k, seq):
+    """DECODE_PROF=1 build, step launches t = 1..15: median wave-0 time (us) of the logit loop, the token
+    phase, and each cell stage m (marks 120 + 24 (t + 1) + {0: after the logit loop, 1: cell start,
+    2 + m: after cell stage m})."""
+    raw = seq.reshape(-1, 4096).cpu().numpy().astype(np.int64) & 0xffffffff
+    ts = raw[:, :1024]
+    rows = {'logit': [], 'token': [], 'cell': []}
+    per_m = [[] for _ in range(20)]
+    for t in range(1, 16):
+        b = 120 + 24 * (t + 1)
+        st = ts[:, 2 * (t + 1)]
+        rows['logit'].append(np.median(((ts[:, b] - st) % (1 << 32)) / 100.0))
+        rows['token'].append(np.median(((ts[:, b + 1] - ts[:, b]) % (1 << 32)) / 100.0))
+        prev = ts[:, b + 1]
+        for m in range(20):
+            cur = ts[:, b + 2 + m]
+            per_m[m].append(np.median(((cur - prev) % (1 << 32)) / 100.0))
+            prev = cur
+        rows['cell'].append(np.median(((ts[:, b + 21] - ts[:, b + 1]) % (1 << 32)) / 100.0))
+    print(k, 'median over t=1..15 (us): logit %.1f token %.1f cell %.1f' % tuple(np.median(rows[x]) for x in
+                                                                                ('logit', 'token', 'cell')))
+    print(k, 'cell stage m (us):', ' '.join('%d:%.2f' % (m, np.median(v)) for m, v in enumerate(per_m)))
+
+
 def main():
     pop = int(os.environ.get('POP', '512'))
     rounds = int(os.environ.get('ROUNDS', '3'))
@@ -92,6 +116,7 @@ def main():
             print('--- %s iteration %d of 3 (decode, CIDEr-D, ranks, noise sum, Adam), queued after a 50 ms idle'
                   % (k, q + 1))
             launch_spans(k, seq)
+            cell_stages(k, seq)
     base = np.median(res['base'])
     out = {k: {'median_ms': round(float(np.median(v)), 3), 'min_ms': round(float(np.min(v)), 3),
                'vs_base': round(float(np.median(v) / base), 3),
