@@ -182,12 +182,13 @@ class EngineWorker:
         if cur is not None and not same:
             self.policy.set_model(cur)
             self._cur = (task_id, cur)
+            self._cur_version = getattr(self, '_cur_version', 0) + 1
         if task_data.batch_data is not None:
             self.policy._ensure_batch(task_data.batch_data)
         if self.mutator is not None and self.mutator.active:
             # calc_sensitivity of the task's theta on its batch before evolve (nic_nes_worker.py:137-142)
             from .mutations import batch_fc
-            self.mutator.prepare((task_id, getattr(self, '_cur', None)), self.e.theta()[1], batch_fc(task_data.batch_data))
+            self.mutator.prepare((task_id, getattr(self, '_cur_version', 0)), self.e.theta()[1], batch_fc(task_data.batch_data))
 
     def fitness_batch(self, task_id, task_data, member_begin, count):
         """-> list of NESResult(fitness=[f+, f-] fp64, noise_idx, member)."""

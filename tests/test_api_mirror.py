@@ -473,3 +473,18 @@ def test_epoch_counts_loader_wraps(workload):
     m = M.EngineMaster(spec, _engine(workload))
     m.run(Wrapping(), max_iterations=4)
     assert m.sched.epoch == 1 + 2            # the run's own pass + wraps after batches 2 and 4
+
+
+def test_mutation_worker_with_state_dict_models(workload):
+    """EngineWorker with a mutation and tasks whose `current` is a state_dict (not a path): the per-task
+    cache key must not compare tensors."""
+    from nicnes import nes as NN
+    dims, theta, fc, gts, df, n, table = workload
+    e = _engine(workload)
+    spec = _mut_spec(2, 'SM-PROPORTIONAL')
+    w = N.EngineWorker(e, spec, worker_id=1)
+    sd = NN.state_dict_from_vector(torch.from_numpy(theta), NN.param_shapes(e))
+    batch = {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts}
+    for tid in (1, 2):
+        res = w.fitness_batch(tid, N.NESTask(current=sd, batch_data=batch, noise_stdev=0.05, iteration=tid), 0, 2)
+        assert len(res) == 2 and e.mutation[0] == 'scale'
