@@ -136,6 +136,9 @@ def main():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--pop-per-gpu', type=int, default=512)
     ap.add_argument('--batch', type=int, default=128)
+    ap.add_argument('--theta-gain', type=float, default=1.0, help='weight init gain (1: the reference xavier init; '
+                    '4 with --bias-std 0.1: peaked, trained-like logits)')
+    ap.add_argument('--bias-std', type=float, default=0.0)
     ap.add_argument('--batches', type=int, default=1, help='distinct batches per iteration (single_batch: false, '
                     'member i on batch i mod N)')
     ap.add_argument('--sigma', type=float, default=0.01)
@@ -180,7 +183,8 @@ def main():
     P = P_local * world
     eng = nicnes.Engine(max_batch=B, max_members=P_local, noise_len=args.noise_len, noise_seed=0,
                         device=dev)
-    S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu, batches=args.batches)
+    S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu, batches=args.batches,
+                            theta_gain=args.theta_gain, bias_std=args.bias_std)
     eng.set_fitness_mode(args.fitness)
     eng.set_decode_split(args.decode_split, args.decode_rows)
     runner = PopulationRunner(eng, P, args.sigma, l2coeff=1e-7, stepsize=1e-3, rank=rank, world_size=world,
@@ -245,6 +249,8 @@ def main():
                                'images, sigma %.3g, full iteration (decode+CIDEr-D+ranks+noise sum+Adam)'
                                % (P, P_local, B, args.sigma) + (", 'bu' fc features" if args.bu else '')
                                + (', fitness %s' % args.fitness if args.fitness != 'greedy' else '')
+                               + (', theta gain %g bias std %g (not the reference init)' % (args.theta_gain, args.bias_std)
+                                  if (args.theta_gain != 1.0 or args.bias_std) else '')
                                + (', %d batches per iteration (single_batch false: member i on batch i mod %d)'
                                   % (args.batches, args.batches) if args.batches > 1 else ''),
                    'population': P, 'members_per_gpu': P_local, 'batch_size': B, 'batches_per_iteration': args.batches,

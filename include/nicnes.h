@@ -138,7 +138,11 @@ int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begi
 
 /* nicnes_evaluate_lp where member member_begin + k decodes and is scored on batch
  * member_batch_host[k] (a HOST array of count entries in [0, n_batches), copied before return) of
- * the batches set by nicnes_set_batches. NULL = every member on batch 0 (only with one batch held). */
+ * the batches set by nicnes_set_batches. NULL = every member on batch 0 (only with one batch held).
+ * Greedy decodes without log-prob output may bound lse from an exp-sum over pair maxima instead of
+ * summing every exp (same tokens; rows the bound leaves undecided take the exact pass). The engine
+ * switches to the exact sum for the next 32 such decodes when a bounded decode needed >= 2 exact
+ * passes (peaked logits of trained models); env NICNES_BOUNDED_LSE=0 / 1 forces never / always. */
 int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
                             const int32_t* member_batch_host, double* fitness_out, int32_t* seq_out, float* logprob_out,
                             void* stream);

@@ -20,6 +20,7 @@ struct DecodeParams {
     float* part;                 // split path: [members * slabs * S] x PART_FLOATS partial greedy states
     int32_t force_exact;         // test hook (NICNES_FORCE_EXACT=1): every step takes the exact tie pass
     float lse_margin;            // widening of the bounded-lse interval: 2e-3 (test hook NICNES_LSE_MARGIN)
+    int32_t bounded_lse;         // 1: greedy-only decode with the pair-bounded lse (needs lp == NULL)
     int32_t B, F, V1, T;
     int32_t G;                   // row groups per slab: 4 (128-row slabs) or 2 (64-row slabs)
     int32_t S;                   // logit workgroups per member slab (1 + G = 4: the fused step kernel)

@@ -500,6 +500,10 @@ __device__ __forceinline__ void epilogue64(RowState& st, const f32x16& P0, const
             records_scan(st, P0, vbase);
             records_scan(st, P1, vbase + 32);
         }
+        // a stage whose every pair maximum lies 24 below the running max adds < 2^-34 of the max term per
+        // logit to the sum: dropping it keeps s a lower bound, and the whole vocabulary's dropped mass
+        // (< 4e-7 of s) stays far inside the 2e-3 margin of tie_window (peaked, trained-model logits)
+        if (__all(tmax < st.m - 24.f)) return;
         const float mnew = vmax2(st.m, tmax);
         const float ml = mnew * LOG2E;
         float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
@@ -622,6 +626,7 @@ __device__ __forceinline__ void epilogue32(RowState& st, const f32x16& P0, int v
         for (int r = 0; r < 8; ++r) q[r] = vmax2(P0[2 * r], P0[2 * r + 1]);
         const float tmax = vmax3(vmax3(q[0], q[1], q[2]), vmax3(q[3], q[4], q[5]), vmax2(q[6], q[7]));
         if (__any(tmax > st.r1v)) records_scan(st, P0, vbase);
+        if (__all(tmax < st.m - 24.f)) return;                    // see epilogue64
         const float mnew = vmax2(st.m, tmax);
         const float ml = mnew * LOG2E;
         float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
@@ -1144,7 +1149,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
         float m = 0.f, lse = 0.f;
         int tok = 0x7fffffff;
         bool ovf = false;
-        const bool pairs = p.lp == nullptr;        // the logit kernel ran its PAIRS variant
+        const bool pairs = p.bounded_lse && p.lp == nullptr;   // the logit kernel ran its PAIRS variant
         TieWindow w = tie_window(1.f, false, 0.f);
         if (folder) {
             const int nh = G == 4 ? 1 : 2, nk = p.S * nh;     // partial k = q * nh + f, in (q, f) order
@@ -1371,9 +1376,9 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
         }
     };
     const dim3 block(NTHREADS);
-    // greedy-only decodes (no log-prob output) bound lse by pair maxima (PAIRS); with p->lp the exact
-    // exp-sum gives seq_logprobs
-    const bool pairs = p->lp == nullptr;
+    // greedy-only decodes (no log-prob output) may bound lse by pair maxima (PAIRS, the engine decides:
+    // nicnes_evaluate_batches); with p->lp the exact exp-sum gives seq_logprobs
+    const bool pairs = p->bounded_lse && p->lp == nullptr;
     mark(0);
     if (fused) {
         hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(1, member_count, nslabs), block, LDS32, stream, *p);

@@ -102,6 +102,16 @@ struct nicnes_handle {
     bool timing = false;
     int force_exact = 0;      // test hook: exact tie pass on every step (NICNES_FORCE_EXACT=1)
     float lse_margin = 2e-3f; // bounded-lse margin; test hook NICNES_LSE_MARGIN widens it (more undecided rows)
+    // bounded-lse policy: greedy-only decodes use the pair-bounded lse unless the previous bounded decode
+    // sent rows to the exact pass (peaked, trained-model logits put lse near binade edges); then the
+    // next exact_span decodes sum the exp exactly. The fallback counter is read back asynchronously.
+    int bounded_mode = 2;     // NICNES_BOUNDED_LSE: 0 never, 1 always, 2 adaptive
+    int exact_left = 0;
+    int last_bounded = 0;
+    int32_t fb_seen = 0;
+    int32_t* stats_host = nullptr;
+    hipEvent_t stats_ev = nullptr;
+    bool stats_pending = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     hipEvent_t dev[DECODE_MAX_EVENTS] = {};   // between the decode's launches (phase split)
     int dev_kind[DECODE_MAX_EVENTS] = {};     // kind of the launch each event follows (DK_*)
@@ -300,6 +310,8 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
         h->force_exact = (fe && fe[0] == '1') ? 1 : 0;
         const char* lm = getenv("NICNES_LSE_MARGIN");
         if (lm && lm[0]) h->lse_margin = (float)atof(lm);
+        const char* bl = getenv("NICNES_BOUNDED_LSE");
+        if (bl && (bl[0] == '0' || bl[0] == '1')) h->bounded_mode = bl[0] - '0';
     }
     {
         int ncu = 0;
@@ -308,6 +320,10 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
     }
     if (!rc && nicnes_decode_init() != hipSuccess) rc = fail(h, NICNES_ERR_HIP, "nicnes_decode_init");
     if (!rc) rc = dalloc(h, &h->stats, 4);
+    if (!rc && hipHostMalloc((void**)&h->stats_host, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
+        rc = fail(h, NICNES_ERR_HIP, "hipHostMalloc");
+    if (!rc && hipEventCreateWithFlags(&h->stats_ev, hipEventDisableTiming) != hipSuccess)
+        rc = fail(h, NICNES_ERR_HIP, "hipEventCreate");
     if (!rc) rc = dalloc(h, &h->partials, 2 * (size_t)nicnes_adam_blocks(h->D));
     if (!rc) rc = dalloc(h, &h->norms, 2);
     if (!rc) {
@@ -344,6 +360,9 @@ int nicnes_destroy(nicnes_handle* h) {
                     h->rank_key, h->rank_idx, h->mbatch, h->mut_vec, h->dbuf, h->didx, h->noise_sc};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
+    if (h->stats_pending) (void)hipEventSynchronize(h->stats_ev);
+    if (h->stats_host) (void)hipHostFree(h->stats_host);
+    if (h->stats_ev) (void)hipEventDestroy(h->stats_ev);
     for (hipEvent_t e : h->ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->dev)
@@ -636,6 +655,15 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     p.alive = h->alive;
     p.force_exact = h->force_exact;
     p.lse_margin = h->lse_margin;
+    if (h->stats_pending && hipEventQuery(h->stats_ev) == hipSuccess) {   // the last decode's fallbacks
+        const int32_t fb = h->stats_host[0];
+        if (h->last_bounded && fb - h->fb_seen >= 2) h->exact_left = 32;
+        h->fb_seen = fb;
+        h->stats_pending = false;
+    }
+    bool bounded = h->bounded_mode == 1 || (h->bounded_mode == 2 && h->exact_left == 0);
+    if (h->bounded_mode == 2 && h->exact_left > 0 && !p.lp) --h->exact_left;
+    p.bounded_lse = bounded ? 1 : 0;
     int G = 0, nslabs = 0, S = 0;
     decode_shape(h, h->B, count, &G, &nslabs, &S);
     if ((int64_t)count * nslabs * S > h->part_cap)
@@ -667,6 +695,12 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     HIPC(h, nicnes_launch_decode(&p, count, nslabs, s, h->timing ? h->dev : nullptr, h->dev_kind, &n_ev));
     h->n_dev = h->timing ? n_ev : 0;
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
+    if (!h->stats_pending) {          // read the fallback counter back without a host wait
+        HIPC(h, hipMemcpyAsync(h->stats_host, h->stats, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIPC(h, hipEventRecord(h->stats_ev, s));
+        h->stats_pending = true;
+        h->last_bounded = bounded && !p.lp;
+    }
     CiderTables tb = tables_of(h);
     if (h->img_tables)
         HIPC(h, nicnes_launch_cider_img(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,

@@ -104,7 +104,7 @@ def build_references(base_captions, vocab_size, seed=4321, n_refs=5, df_sets=409
 
 
 def setup_engine_workload(engine, B=128, theta_seed=0, fc_seed=1234, bu=False, noise=None, ref_seed=4321,
-                          df_sets=4096, batches=1):
+                          df_sets=4096, batches=1, theta_gain=1.0, bias_std=0.0):
     """Load a full synthetic workload into an Engine: noise table, theta, fc, refs + df.
     batches > 1: that many batches of B images each (per-member batches, single_batch: false), held
     with set_batches; fc / gts / base then cover all batches * B images in batch order.
@@ -114,7 +114,7 @@ def setup_engine_workload(engine, B=128, theta_seed=0, fc_seed=1234, bu=False, n
     if noise is None:
         noise = noise_table(engine.cfg.noise_len)
     engine.set_noise_table(noise)
-    theta = init_theta(dims, theta_seed)
+    theta = init_theta(dims, theta_seed, theta_gain, bias_std)
     engine.set_theta(theta)
     n = B * batches
     fc = fc_feats(n, dims.F, fc_seed, bu)
