@@ -932,18 +932,31 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
                          win_state(__shfl_xor(st.ev, 32), m, w) != 0;
         if (__syncthreads_or(ovf ? 1 : 0)) {
             // rare: more records than tracked fall in the tie window (or, PAIRS mode, the bounds on
-            // lse leave a record undecided) -> exact pass: the exp-sum first if PAIRS, then the first
-            // id in the window
+            // lse leave a record undecided) -> exact pass. PAIRS: the exp-sum sweep first, then the
+            // records decide as in the exact mode, and only an evicted record in the window needs the
+            // sweep for the first id in the window
             int best = 0x7fffffff;
             float ssum = 0.f;
+            bool find = true;
             if (PAIRS) {
                 exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, true, true, m, 0.f,
                             ssum, best);
                 lse = logf(ssum + __shfl_xor(ssum, 32));
+                const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
+                const int ci[4] = {st.r0i, st.r1i, __shfl_xor(st.r0i, 32), __shfl_xor(st.r1i, 32)};
+                int t2 = 0x7fffffff;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (in_window(cv[k], m, lse) && ci[k] < t2) t2 = ci[k];
+                const bool ev2 = p.force_exact || in_window(st.ev, m, lse) || in_window(__shfl_xor(st.ev, 32), m, lse);
+                find = __syncthreads_or(ev2 ? 1 : 0) != 0;
+                if (!find) tok = t2;
             }
-            exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, true, false, m, lse,
-                        ssum, best);
-            tok = min(best, __shfl_xor(best, 32));
+            if (find) {
+                exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, true, false, m, lse,
+                            ssum, best);
+                tok = min(best, __shfl_xor(best, 32));
+            }
             if (c.tid == 0) atomicAdd(p.stats + 0, 1);
         }
         // no candidate only when every logit is NaN (torch.max would return a NaN's index):
@@ -1202,17 +1215,38 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
         if (__syncthreads_or((p.force_exact || ovf) ? 1 : 0)) {
             // rare: more records than tracked fall in the tie window, or (PAIRS mode) the bounds on lse
             // leave a record undecided -> exact pass over the whole vocabulary (every workgroup of the
-            // member does it: it needs the token); PAIRS mode sums the exp first
+            // member does it: it needs the token); PAIRS mode sums the exp first and re-decides from the
+            // records, sweeping for the first id only when an evicted record is in the window
             int best = 0x7fffffff;
             float ssum = 0.f;
+            bool find = true;
             if (pairs) {
                 exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, folder, true, m, 0.f,
                             ssum, best);
                 lse = logf(ssum + __shfl_xor(ssum, 32));
+                int t2 = 0x7fffffff;
+                bool ev2 = p.force_exact;
+                if (folder) {
+                    const int nh = G == 4 ? 1 : 2, nk = p.S * nh;
+                    for (int k = 0; k < nk; ++k) {
+                        const float* pb = part_ptr(p, c.wg, k / nh, c.wave + k % nh) + c.lane;
+                        const float r0v = pb[128], r1v = pb[256];
+                        const int r0i = __builtin_bit_cast(int, pb[192]), r1i = __builtin_bit_cast(int, pb[320]);
+                        if (in_window(r0v, m, lse) && r0i < t2) t2 = r0i;
+                        if (in_window(r1v, m, lse) && r1i < t2) t2 = r1i;
+                        ev2 = ev2 || in_window(pb[384], m, lse);
+                    }
+                    t2 = min(t2, __shfl_xor(t2, 32));
+                    ev2 = ev2 || (__shfl_xor(ev2 ? 1 : 0, 32) != 0);
+                }
+                find = __syncthreads_or(ev2 ? 1 : 0) != 0;
+                if (!find) tok = t2;
             }
-            exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, folder, false, m, lse,
-                        ssum, best);
-            tok = min(best, __shfl_xor(best, 32));
+            if (find) {
+                exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, folder, false, m, lse,
+                            ssum, best);
+                tok = min(best, __shfl_xor(best, 32));
+            }
             if (lead) atomicAdd(p.stats + 0, 1);
         }
         if (tok >= p.V1) tok = 0;               // every logit NaN: end the caption (fused kernel rule)
