@@ -17,6 +17,8 @@ timeout -k 10 200 python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --
 # per-GPU shapes of the multi-GPU configs: configs[3] pop=2048 / 8 GPUs, configs[4] bu pop=512 / 8 GPUs
 timeout -k 10 200 python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --pop-per-gpu 256 > $O/bench_p256.json 2> $O/bench_p256.err
 timeout -k 10 200 python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --pop-per-gpu 64 --bu > $O/bench_p64_bu.json 2> $O/bench_p64_bu.err
+# peaked, trained-like logits (theta gain 4, bias std 0.1): the adaptive bounded-lse policy
+timeout -k 10 200 python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --theta-gain 4 --bias-std 0.1 > $O/bench_trained_like_theta.json 2> $O/bench_trained_like_theta.err
 # single_batch: false (mscoco_nes.json's default): 64 distinct batches, member i on batch i mod 64
 timeout -k 10 300 python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --batches 64 > $O/bench_batches64.json 2> $O/bench_batches64.err
 echo done
