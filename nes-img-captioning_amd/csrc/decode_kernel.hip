@@ -500,10 +500,6 @@ __device__ __forceinline__ void epilogue64(RowState& st, const f32x16& P0, const
             records_scan(st, P0, vbase);
             records_scan(st, P1, vbase + 32);
         }
-        // a stage whose every pair maximum lies 24 below the running max adds < 2^-34 of the max term per
-        // logit to the sum: dropping it keeps s a lower bound, and the whole vocabulary's dropped mass
-        // (< 4e-7 of s) stays far inside the 2e-3 margin of tie_window (peaked, trained-model logits)
-        if (__all(tmax < st.m - 24.f)) return;
         const float mnew = vmax2(st.m, tmax);
         const float ml = mnew * LOG2E;
         float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
@@ -626,7 +622,6 @@ __device__ __forceinline__ void epilogue32(RowState& st, const f32x16& P0, int v
         for (int r = 0; r < 8; ++r) q[r] = vmax2(P0[2 * r], P0[2 * r + 1]);
         const float tmax = vmax3(vmax3(q[0], q[1], q[2]), vmax3(q[3], q[4], q[5]), vmax2(q[6], q[7]));
         if (__any(tmax > st.r1v)) records_scan(st, P0, vbase);
-        if (__all(tmax < st.m - 24.f)) return;                    // see epilogue64
         const float mnew = vmax2(st.m, tmax);
         const float ml = mnew * LOG2E;
         float s = st.s * __builtin_amdgcn_exp2f((st.m - mnew) * LOG2E);
