@@ -223,7 +223,14 @@ def main():
     # averages over the same launches)
     ph = phases[-1]
     G, nslabs, S_split = eng.decode_shape(B, P_local)
-    if ph['step_launches']:
+    if not ph['step_launches'] and not ph['logit_launches']:
+        # two-stream decode (NICNES_DECODE_STREAMS=2): the halves' launches overlap, so the whole decode
+        # is the measured unit
+        kname, n_step = 'decode (img + step/logit/cell kernels, 2 streams)', 1
+        step_ms = float(np.mean(dec_ms))
+        step_flop = flops
+        alg_bytes = step_noise_bytes_per_member(B) * P_local
+    elif ph['step_launches']:
         kname, n_step = 'nicnes_decode_step_kernel', ph['step_launches']
         step_ms = float(np.mean([q['step_ms'] for q in phases])) / n_step
         step_flop = step_flops_per_member(B) * P_local / n_step

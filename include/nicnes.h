@@ -224,6 +224,13 @@ int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host);
 int nicnes_set_decode_split(nicnes_handle* h, int32_t S, int32_t G);
 /* the shape an evaluate of `count` members of a B-image batch would use: [0] G, [1] slabs, [2] S */
 int nicnes_decode_shape(nicnes_handle* h, int32_t B, int32_t count, int32_t* out3_host);
+/* Decode streams (not a reference interface): the evaluate's members split evenly over n streams, the
+ * caller's and n - 1 engine streams joined back into the caller's before the CIDEr-D launch, so that one
+ * part's launches fill the CUs the others' launch gaps leave idle. n = 0 picks automatically (2 on the
+ * split path, 1 on the fused path), 1..4 forces; env NICNES_DECODE_STREAMS sets the initial value. A
+ * multi-stream decode records no per-launch events (nicnes_decode_phase_times reports zeros).
+ * Tokens do not depend on n. */
+int nicnes_set_decode_streams(nicnes_handle* h, int32_t n);
 
 #ifdef __cplusplus
 }

@@ -40,6 +40,9 @@ struct DecodeParams {
 // in *n_launch.
 #define DECODE_MAX_EVENTS 64
 extern "C" hipError_t nicnes_decode_init();
+// shifts the per-member and per-workgroup pointers of *p to member m0 (a decode of members m0.. on
+// its own stream; nslabs = the launch's row slabs)
+extern "C" void nicnes_decode_shift(DecodeParams* p, int m0, int nslabs);
 extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,
                                            hipEvent_t* evs, int* kinds, int* n_launch);
 // lane scratch for up to member_count members x row_waves 32-row waves of one sign

@@ -71,7 +71,9 @@ __device__ __forceinline__ void wave_prio(int wave) {
 #define DECODE_PROF 0      // timing-only build: per-workgroup start/end s_memrealtime (100 MHz) of every
 #endif                     // launch written over seq[wg * 4096 + slot] (wrong tokens; scripts/ablate.py)
 #if DECODE_PROF
-#define PROF_MARK(slot)                                                                          \
+// (wgi, stride): the fused path keeps 4096 ints per workgroup (one per member: seq holds 2*B*T ints per
+// member); the split path 1024 per workgroup (S * slabs <= 4 workgroups per member, slots < 256)
+#define PROF_AT(wgi, stride, slot)                                                               \
     do {                                                                                         \
         if (threadIdx.x == 0) {                                                                  \
             unsigned long long t_, k_;                                                           \
@@ -79,14 +81,17 @@ __device__ __forceinline__ void wave_prio(int wave) {
             unsigned hw_, xcc_;                                                                  \
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                     \
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                   \
-            int32_t* q_ = p.seq + (size_t)(blockIdx.x * gridDim.y + blockIdx.y) * 4096;          \
+            int32_t* q_ = p.seq + (size_t)(wgi) * (stride);                                      \
             q_[(slot)] = (int32_t)(uint32_t)t_;                                                  \
-            q_[2048 + (slot)] = (int32_t)(((xcc_ & 15u) << 16) | ((hw_ >> 8) & 0xffffu));         \
-            q_[1024 + (slot)] = (int32_t)(uint32_t)k_;                                           \
+            q_[(stride) / 2 + (slot)] = (int32_t)(((xcc_ & 15u) << 16) | ((hw_ >> 8) & 0xffffu)); \
+            q_[(stride) / 4 + (slot)] = (int32_t)(uint32_t)k_;                                   \
         }                                                                                        \
     } while (0)
+#define PROF_MARK(slot) PROF_AT(blockIdx.x * gridDim.y + blockIdx.y, 4096, slot)
+#define PROF_SPLIT(slot) PROF_AT((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, 1024, slot)
 #else
 #define PROF_MARK(slot) do { } while (0)
+#define PROF_SPLIT(slot) do { } while (0)
 #endif
 
 // lane id recomputed at the point of use (volatile: never hoisted or kept live across a loop)
@@ -815,7 +820,8 @@ template <int G>
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParams p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SCtx<G> c = make_sctx<G>(p);
-    PROF_MARK(80);
+    const bool fused_path = G == 4 && p.S == 1;
+    if (fused_path) PROF_MARK(80); else PROF_SPLIT(250);
     const float* fcm = p.fc + (p.member_batch ? (size_t)p.member_batch[c.member] * p.B * p.F : 0);
     const rsrc_t fc_r = make_rsrc(fcm, 4u * (uint32_t)p.B * (uint32_t)p.F);
     const uint32_t lo = 4u * c.lane;
@@ -861,7 +867,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
         st1(c.scr_r, lo, U_SLOT, 1.0f);
     }
     if (c.q == 0 && c.tid == 0) p.alive[c.wg] = 1;
-    PROF_MARK(81);
+    if (fused_path) PROF_MARK(81); else PROF_SPLIT(251);
 }
 
 // ========== step kernel: logits + greedy token of step t, then the LSTM cell of step t+1 ========
@@ -1091,6 +1097,7 @@ template <int G, bool PAIRS>
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_logit_kernel(DecodeParams p, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SCtx<G> c = make_sctx<G>(p);
+    PROF_SPLIT(2 * t - 2);
     if (t > 1 && p.alive2[((t - 1) & 1) * p.alive_stride + c.wg] == 0) return;
     const uint32_t lo = 4u * c.lane;
     const int nst = (p.V1 + 63) >> 6, S = (int)gridDim.x;
@@ -1112,6 +1119,25 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_logit_kernel(DecodePar
     pb[256] = st.r1v;
     pb[320] = __builtin_bit_cast(float, st.r1i);
     pb[384] = st.ev;
+    PROF_SPLIT(2 * t - 1);
+}
+
+// partials k0 .. k0+7 of a row (those < nk: the merge skips the others)
+struct Part8 {
+    float m[8], s[8], r0v[8], r1v[8], ev[8];
+    int r0i[8], r1i[8];
+};
+__device__ __forceinline__ void load_part8(const DecodeParams& p, int wg, int wave, int lane, int nh, int nk, int k0,
+                                           Part8& o) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+        if (k0 + u < nk) {                        // uniform: no load for the absent partials
+            const int k = k0 + u;
+            const float* pb = part_ptr(p, wg, k / nh, wave + k % nh) + lane;
+            o.m[u] = pb[0]; o.s[u] = pb[64];
+            o.r0v[u] = pb[128]; o.r1v[u] = pb[256]; o.ev[u] = pb[384];
+            o.r0i[u] = __builtin_bit_cast(int, pb[192]); o.r1i[u] = __builtin_bit_cast(int, pb[320]);
+        }
 }
 
 template <int G>
@@ -1119,22 +1145,14 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const SCtx<G> c = make_sctx<G>(p);
     const bool lead = c.q == 0 && c.tid == 0;
+    [[maybe_unused]] const int pb0 = 32 + 12 * (t + 1);   // DECODE_PROF slots: start, merged, staged, 5 tiles, end
+    PROF_SPLIT(pb0);
     if (t > 1 && p.alive2[((t - 1) & 1) * p.alive_stride + c.wg] == 0) {
         if (lead) p.alive2[(t & 1) * p.alive_stride + c.wg] = 0;   // keep the parity chain current
         return;
     }
     const uint32_t lo = 4u * c.lane;
     const bool folder = G == 4 || c.hf == 0;       // waves that own the rows' token and the cell fold
-    float hB[64];
-    if (t < 0) {
-#pragma unroll
-        for (int i = 0; i < 64; ++i) hB[i] = 0.f;               // h = 0 before the first cell
-    } else {
-#pragma unroll
-        for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, HP_SLOT(t & 1, i));
-    }
-#pragma unroll
-    for (int i = 0; i < 64; ++i) pin(hB[i]);
     const uint32_t ib = (uint32_t)p.off_i2h_b, hb = (uint32_t)p.off_h2h_b, bmin = min(ib, hb);
     auto csrc = [&](int m) {                                     // gate tile m: i2h rows | h2h rows
         const uint32_t r = gate_row(m);
@@ -1148,9 +1166,32 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
         return Sx;
     };
     const int nb = 4 / (int)gridDim.x, m0 = 5 * nb * c.q, m1 = m0 + 5 * nb;
+    const int nh = G == 4 ? 1 : 2, nk = p.S * nh;             // partial k = q * nh + f, in (q, f) order
+    // load order = order of need: the first 8 partials of the rows, the first gate tile, then h (after
+    // the merge). vmcnt retires in issue order and counts at most 63 loads: a load issued ahead of the
+    // partials, or more than 63 behind them, would make the merge wait for the 64 KB tile
+    PROF_SPLIT(pb0 + 8);
+    Part8 pre;
+    if (t >= 1 && folder) load_part8(p, c.wg, c.wave, c.lane, nh, nk, 0, pre);
+#if DECODE_PROF
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PROF_SPLIT(pb0 + 9);
+#endif
     Stage64Regs s64;
     // the first gate tile's rows do not depend on the token: their loads fly during the merge
     if (t < p.T) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
+    float hB[64];
+    auto load_h = [&]() {
+        if (t < 0) {
+#pragma unroll
+            for (int i = 0; i < 64; ++i) hB[i] = 0.f;           // h = 0 before the first cell
+        } else {
+#pragma unroll
+            for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, HP_SLOT(t & 1, i));
+        }
+#pragma unroll
+        for (int i = 0; i < 64; ++i) pin(hB[i]);
+    };
     int it = 0;                                   // token fed to the next cell (0 = BOS at t = 0)
     if (t >= 1) {
         // ---- merge the S partial states of each row (lane halves combined last, as the fused kernel)
@@ -1160,22 +1201,15 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
         const bool pairs = p.bounded_lse && p.lp == nullptr;   // the logit kernel ran its PAIRS variant
         TieWindow w = tie_window(1.f, false, 0.f);
         if (folder) {
-            const int nh = G == 4 ? 1 : 2, nk = p.S * nh;     // partial k = q * nh + f, in (q, f) order
             float mh = -1.0e30f, sh = 0.f;
             for (int k0 = 0; k0 < nk; k0 += 8) {              // every load of 8 partials issued before use
-                float pm[8], ps[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int k = min(k0 + u, nk - 1);
-                    const float* pb = part_ptr(p, c.wg, k / nh, c.wave + k % nh) + c.lane;
-                    pm[u] = pb[0];
-                    ps[u] = pb[64];
-                }
+                Part8 cur;
+                if (k0 == 0) cur = pre; else load_part8(p, c.wg, c.wave, c.lane, nh, nk, k0, cur);
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
                     if (k0 + u < nk) {
-                        const float mn = fmaxf(mh, pm[u]);
-                        sh = sh * __builtin_amdgcn_exp2f((mh - mn) * LOG2E) + ps[u] * __builtin_amdgcn_exp2f((pm[u] - mn) * LOG2E);
+                        const float mn = fmaxf(mh, cur.m[u]);
+                        sh = sh * __builtin_amdgcn_exp2f((mh - mn) * LOG2E) + cur.s[u] * __builtin_amdgcn_exp2f((cur.m[u] - mn) * LOG2E);
                         mh = mn;
                     }
             }
@@ -1186,27 +1220,22 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
             w = tie_window(stot, pairs, p.lse_margin);
             lse = w.lse;
             for (int k0 = 0; k0 < nk; k0 += 8) {
-                float r0v[8], r1v[8], ev[8];
-                int r0i[8], r1i[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int k = min(k0 + u, nk - 1);
-                    const float* pb = part_ptr(p, c.wg, k / nh, c.wave + k % nh) + c.lane;
-                    r0v[u] = pb[128]; r1v[u] = pb[256]; ev[u] = pb[384];
-                    r0i[u] = __builtin_bit_cast(int, pb[192]); r1i[u] = __builtin_bit_cast(int, pb[320]);
-                }
+                Part8 cur;
+                if (k0 == 0) cur = pre; else load_part8(p, c.wg, c.wave, c.lane, nh, nk, k0, cur);
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
                     if (k0 + u < nk) {
-                        const int w0 = win_state(r0v[u], m, w), w1 = win_state(r1v[u], m, w);
-                        if (w0 == 1 && r0i[u] < tok) tok = r0i[u];
-                        if (w1 == 1 && r1i[u] < tok) tok = r1i[u];
-                        ovf = ovf || w0 == 2 || w1 == 2 || win_state(ev[u], m, w) != 0;
+                        const int w0 = win_state(cur.r0v[u], m, w), w1 = win_state(cur.r1v[u], m, w);
+                        if (w0 == 1 && cur.r0i[u] < tok) tok = cur.r0i[u];
+                        if (w1 == 1 && cur.r1i[u] < tok) tok = cur.r1i[u];
+                        ovf = ovf || w0 == 2 || w1 == 2 || win_state(cur.ev[u], m, w) != 0;
                     }
             }
             tok = min(tok, __shfl_xor(tok, 32));
             ovf = ovf || (__shfl_xor(ovf ? 1 : 0, 32) != 0);
         }
+        PROF_SPLIT(pb0 + 10);
+        load_h();
         if (__syncthreads_or((p.force_exact || ovf) ? 1 : 0)) {
             // rare: more records than tracked fall in the tie window, or (PAIRS mode) the bounds on lse
             // leave a record undecided -> exact pass over the whole vocabulary (every workgroup of the
@@ -1222,7 +1251,6 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
                 int t2 = 0x7fffffff;
                 bool ev2 = p.force_exact;
                 if (folder) {
-                    const int nh = G == 4 ? 1 : 2, nk = p.S * nh;
                     for (int k = 0; k < nk; ++k) {
                         const float* pb = part_ptr(p, c.wg, k / nh, c.wave + k % nh) + c.lane;
                         const float r0v = pb[128], r1v = pb[256];
@@ -1246,18 +1274,26 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
         }
         if (tok >= p.V1) tok = 0;               // every logit NaN: end the caption (fused kernel rule)
         const size_t o = (((size_t)c.member * 2 + c.sgn) * p.B + c.bc) * p.T + (t - 1);
+#if DECODE_PROF
+        const bool prev_unf = true;             // timing build: seq holds the marks
+#else
         const bool prev_unf = t == 1 || p.seq[o - 1] != 0;
+#endif
         const bool unfinished = prev_unf && tok > 0;
         it = unfinished ? tok : 0;
+#if !DECODE_PROF
         if (c.q == 0 && folder && c.hh == 0 && c.row_valid) {
             p.seq[o] = it;
             if (p.lp) p.lp[o] = -lse;           // seq_logprobs[:, t-1] (nets.py:208,241)
         }
+#endif
         const int any = __syncthreads_or((folder && unfinished && c.row_valid) ? 1 : 0);
         if (lead) p.alive2[(t & 1) * p.alive_stride + c.wg] = any;
         if (!any) return;                       // the reference stops here (nets.py:242-243)
-    } else if (t == 0) {
-        if (lead) p.alive2[c.wg] = 1;           // parity slot 0 read by step 1
+        PROF_SPLIT(pb0 + 1);
+    } else {
+        load_h();
+        if (t == 0 && lead) p.alive2[c.wg] = 1;   // parity slot 0 read by step 1
     }
     if (t >= p.T) return;
 
@@ -1288,6 +1324,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
     const int hpar = (t + 1) & 1;
     stage64_store(lds, 64, c.wave * 64 + lane_fresh(), s64);
     __syncthreads();
+    PROF_SPLIT(pb0 + 2);
     f32x16 hold;
     auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) {
         const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
@@ -1360,7 +1397,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
             if (m + 1 < m1) stage64_store(lds + ((m - m0 + 1) & 1) * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
             __syncthreads();
         }
+        if (m - m0 < 5) PROF_SPLIT(pb0 + 3 + (m - m0));
     }
+    PROF_SPLIT(pb0 + 11);
 }
 
 namespace {
@@ -1388,6 +1427,19 @@ extern "C" hipError_t nicnes_decode_init() {
         if (e != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+extern "C" void nicnes_decode_shift(DecodeParams* p, int m0, int nslabs) {
+    const size_t wg0 = (size_t)m0 * (size_t)nslabs;        // workgroup index wg = member * slabs + slab
+    const size_t rows = (size_t)m0 * 2 * (size_t)p->B * (size_t)p->T;
+    p->noise_idx += m0;
+    if (p->member_batch) p->member_batch += m0;
+    p->seq += rows;
+    if (p->lp) p->lp += rows;
+    p->scratch += wg0 * (size_t)(2 * p->G) * (SCR_SLOTS * 64);   // make_ctx / make_sctx lane scratch
+    p->alive += wg0;
+    p->alive2 += wg0;
+    p->part += wg0 * (size_t)p->S * PART_FLOATS;                 // part_ptr
 }
 
 extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,

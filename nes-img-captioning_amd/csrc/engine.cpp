@@ -92,6 +92,13 @@ struct nicnes_handle {
     int64_t part_cap = 0;             // in logit workgroups (members x slabs x S)
     int n_cu = 256;
     int dec_S = 0, dec_G = 0;         // nicnes_set_decode_split (0 = automatic)
+    // the decode's members in n parts on n streams (nicnes_set_decode_streams, NICNES_DECODE_STREAMS;
+    // 0 = automatic: 2 on the split path, 1 on the fused path): one part's launches fill the CUs the
+    // others' launch gaps and tails leave idle
+    int dec_streams = 0;
+    hipStream_t sx[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr;
+    hipEvent_t ev_join[3] = {nullptr, nullptr, nullptr};
     double* partials = nullptr;
     double* norms = nullptr;
 
@@ -116,6 +123,7 @@ struct nicnes_handle {
     hipEvent_t dev[DECODE_MAX_EVENTS] = {};   // between the decode's launches (phase split)
     int dev_kind[DECODE_MAX_EVENTS] = {};     // kind of the launch each event follows (DK_*)
     int n_dev = 0;                            // events recorded by the last timed decode
+    bool multi_stream = false;                // the last decode ran on several streams
 };
 
 namespace {
@@ -312,6 +320,8 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
         if (lm && lm[0]) h->lse_margin = (float)atof(lm);
         const char* bl = getenv("NICNES_BOUNDED_LSE");
         if (bl && (bl[0] == '0' || bl[0] == '1')) h->bounded_mode = bl[0] - '0';
+        const char* ds = getenv("NICNES_DECODE_STREAMS");
+        if (ds && ds[0] >= '1' && ds[0] <= '4' && ds[1] == 0) h->dec_streams = ds[0] - '0';
     }
     {
         int ncu = 0;
@@ -367,6 +377,14 @@ int nicnes_destroy(nicnes_handle* h) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->dev)
         if (e) (void)hipEventDestroy(e);
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    for (int i = 0; i < 3; ++i) {
+        if (h->ev_join[i]) (void)hipEventDestroy(h->ev_join[i]);
+        if (h->sx[i]) {
+            (void)hipStreamSynchronize(h->sx[i]);
+            (void)hipStreamDestroy(h->sx[i]);
+        }
+    }
     delete h;
     return NICNES_OK;
 }
@@ -692,8 +710,34 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     if (p.lp) HIPC(h, hipMemsetAsync(p.lp, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(float), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
     int n_ev = 0;
-    HIPC(h, nicnes_launch_decode(&p, count, nslabs, s, h->timing ? h->dev : nullptr, h->dev_kind, &n_ev));
+    const int nstr = std::min(count, h->dec_streams ? h->dec_streams : ((G == 4 && S == 1) ? 1 : 2));
+    if (nstr > 1) {
+        // members split evenly over the caller's stream and nstr - 1 engine streams; the parts share
+        // nothing but the fallback counter (an atomic). No per-launch events: the launches overlap
+        if (!h->ev_fork) HIPC(h, hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+        for (int i = 0; i < nstr - 1; ++i)
+            if (!h->sx[i]) {
+                HIPC(h, hipStreamCreateWithFlags(&h->sx[i], hipStreamNonBlocking));
+                HIPC(h, hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming));
+            }
+        HIPC(h, hipEventRecord(h->ev_fork, s));
+        for (int i = 0; i < nstr; ++i) {
+            const int a = (int)((int64_t)count * i / nstr), b = (int)((int64_t)count * (i + 1) / nstr);
+            DecodeParams pi = p;
+            nicnes_decode_shift(&pi, a, nslabs);
+            hipStream_t si = i == 0 ? s : h->sx[i - 1];
+            if (i > 0) HIPC(h, hipStreamWaitEvent(si, h->ev_fork, 0));
+            HIPC(h, nicnes_launch_decode(&pi, b - a, nslabs, si, nullptr, nullptr, nullptr));
+        }
+        for (int i = 0; i < nstr - 1; ++i) {
+            HIPC(h, hipEventRecord(h->ev_join[i], h->sx[i]));
+            HIPC(h, hipStreamWaitEvent(s, h->ev_join[i], 0));
+        }
+    } else {
+        HIPC(h, nicnes_launch_decode(&p, count, nslabs, s, h->timing ? h->dev : nullptr, h->dev_kind, &n_ev));
+    }
     h->n_dev = h->timing ? n_ev : 0;
+    h->multi_stream = nstr > 1;
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     if (!h->stats_pending) {          // read the fallback counter back without a host wait
         HIPC(h, hipMemcpyAsync(h->stats_host, h->stats, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -854,7 +898,12 @@ int nicnes_kernel_times(nicnes_handle* h, float* out2_host) {
 }
 
 int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host) {
-    if (!h || !out8_host || h->n_dev < 3) return NICNES_ERR_INVALID;
+    if (!h || !out8_host) return NICNES_ERR_INVALID;
+    if (h->timing && h->n_dev == 0 && h->multi_stream) {      // multi-stream decode: no per-launch events
+        for (int i = 0; i < 8; ++i) out8_host[i] = 0.f;
+        return NICNES_OK;
+    }
+    if (h->n_dev < 3) return NICNES_ERR_INVALID;
     HIPC(h, hipSetDevice(h->device));
     HIPC(h, hipEventSynchronize(h->dev[h->n_dev - 1]));
     // event k follows launch k. Fused: img, then step(t) for t = -1..T (the first two launches run
@@ -877,6 +926,12 @@ int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host) {
         }
     }
     for (int i = 0; i < 8; ++i) out8_host[i] = o[i];
+    return NICNES_OK;
+}
+
+int nicnes_set_decode_streams(nicnes_handle* h, int32_t n) {
+    if (!h || n < 0 || n > 4) return NICNES_ERR_INVALID;
+    h->dec_streams = n;
     return NICNES_OK;
 }
 

@@ -17,7 +17,7 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_evaluate', 'nicnes_rank_weights', 'nicnes_grad_partial', 'nicnes_adam_step', 'nicnes_stats',
            'nicnes_set_timing', 'nicnes_kernel_times', 'nicnes_decode_phase_times', 'nicnes_sgd_step',
            'nicnes_optimizer_update', 'nicnes_last_ratio', 'nicnes_set_fitness_mode', 'nicnes_evaluate_lp',
-           'nicnes_set_decode_split', 'nicnes_decode_shape', 'nicnes_comm_unique_id', 'nicnes_comm_init',
+           'nicnes_set_decode_split', 'nicnes_decode_shape', 'nicnes_set_decode_streams', 'nicnes_comm_unique_id', 'nicnes_comm_init',
            'nicnes_comm_attach', 'nicnes_comm_destroy', 'nicnes_allgather_fitness', 'nicnes_allreduce_grad',
            'nicnes_noise_vectors', 'nicnes_set_batches', 'nicnes_evaluate_batches', 'nicnes_set_mutation']
 
@@ -78,6 +78,7 @@ def lib(path=None):
         'nicnes_decode_phase_times': (c.c_int, [vp, vp]),
         'nicnes_set_decode_split': (c.c_int, [vp, i32, i32]),
         'nicnes_decode_shape': (c.c_int, [vp, i32, i32, vp]),
+        'nicnes_set_decode_streams': (c.c_int, [vp, i32]),
         'nicnes_comm_unique_id': (c.c_int, [vp]),
         'nicnes_comm_init': (c.c_int, [vp, i32, i32, vp]),
         'nicnes_comm_attach': (c.c_int, [vp, vp]),

@@ -305,6 +305,11 @@ class Engine:
         0 = automatic. Tokens do not depend on it."""
         check(self.L.nicnes_set_decode_split(self.h, int(S), int(G)), self.h, 'set_decode_split')
 
+    def set_decode_streams(self, n=0):
+        """Split the evaluate's members over n streams (0 = automatic: 2 on the split path, 1 fused).
+        Tokens do not depend on it."""
+        check(self.L.nicnes_set_decode_streams(self.h, int(n)), self.h, 'set_decode_streams')
+
     def decode_shape(self, B=None, count=1):
         """(G, slabs, S) an evaluate of `count` members would use."""
         out = (ctypes.c_int32 * 3)()

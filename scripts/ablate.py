@@ -63,6 +63,45 @@ def cell_stages(k, seq):
     print(k, 'cell stage m (us):', ' '.join('%d:%.2f' % (m, np.median(v)) for m, v in enumerate(per_m)))
 
 
+def split_spans(k, seq, S=4):
+    """DECODE_PROF=1 build, split path (64 members, S = 4): per launch span, mean workgroup time and the gap
+    to the previous launch's last workgroup; cell launches t = 1..15 split into merge / stage fill / 5 tiles."""
+    raw = seq.reshape(-1, 1024).cpu().numpy().astype(np.int64) & 0xffffffff
+    ts = raw[:, :256]
+    launches = [('img', 250, 251), ('cell-1', 32, 43), ('cell0', 44, 55)]
+    for t in range(1, 17):
+        launches.append(('logit%d' % t, 2 * t - 2, 2 * t - 1))
+        if t < 16:
+            launches.append(('cell%d' % t, 32 + 12 * (t + 1), 32 + 12 * (t + 1) + 11))
+    t0 = ts[:, 250].min()
+    print(k, 'split launch: start_us span_us wg_mean wg_min wg_max gap_us')
+    prev_end = None
+    for name, a, b in launches:
+        st = ((ts[:, a] - t0) % (1 << 32)) / 100.0
+        en = ((ts[:, b] - t0) % (1 << 32)) / 100.0
+        dur = en - st
+        gap = st.min() - prev_end if prev_end is not None else 0.0
+        print('%-8s %9.1f %8.1f %8.1f %8.1f %8.1f %7.1f' % (name, st.min(), en.max() - st.min(), dur.mean(),
+                                                          dur.min(), dur.max(), gap))
+        prev_end = en.max()
+    sub = [[] for _ in range(4)]
+    for t in range(1, 16):
+        b = 32 + 12 * (t + 1)
+        marks = [b, b + 8, b + 9, b + 10, b + 1]
+        for i in range(4):
+            sub[i].append(np.median(((ts[:, marks[i + 1]] - ts[:, marks[i]]) % (1 << 32)) / 100.0))
+    print(k, 'merge split (us): entry->alive %.1f partials %.1f compute %.1f token+sync %.1f' % tuple(
+        np.median(v) for v in sub))
+    ph = [[] for _ in range(8)]
+    for t in range(1, 16):
+        b = 32 + 12 * (t + 1)
+        marks = [b, b + 1, b + 2, b + 3, b + 4, b + 5, b + 6, b + 7, b + 11]
+        for i in range(8):
+            ph[i].append(np.median(((ts[:, marks[i + 1]] - ts[:, marks[i]]) % (1 << 32)) / 100.0))
+    print(k, 'cell t=1..15 median (us): merge %.1f fill %.1f tiles %s end %.1f' % (
+        np.median(ph[0]), np.median(ph[1]), ' '.join('%.1f' % np.median(v) for v in ph[2:7]), np.median(ph[7])))
+
+
 def main():
     pop = int(os.environ.get('POP', '512'))
     rounds = int(os.environ.get('ROUNDS', '3'))
@@ -115,8 +154,11 @@ def main():
         for q, seq in enumerate(seqs):
             print('--- %s iteration %d of 3 (decode, CIDEr-D, ranks, noise sum, Adam), queued after a 50 ms idle'
                   % (k, q + 1))
-            launch_spans(k, seq)
-            cell_stages(k, seq)
+            if pop <= 64:
+                split_spans(k, seq)
+            else:
+                launch_spans(k, seq)
+                cell_stages(k, seq)
     base = np.median(res['base'])
     out = {k: {'median_ms': round(float(np.median(v)), 3), 'min_ms': round(float(np.min(v)), 3),
                'vs_base': round(float(np.median(v) / base), 3),

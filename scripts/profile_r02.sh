@@ -12,6 +12,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$TAG
 mkdir -p $O
 for P in 512 64; do
+  export NICNES_DECODE_STREAMS=1   # per-kernel figures: one stream (the split path defaults to 2)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats$P -o run --output-format csv -- \
       python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --pop-per-gpu $P $EXTRA > $O/stats$P.log 2>&1
   i=0

@@ -233,3 +233,24 @@ def test_split_forced_ties_follow_oracle(eng, G, S):
             eng.set_decode_split(0, 0)
         oseq, _, fr = O.decode(dims, th, fc)
         assert _mismatch(seq.cpu().numpy()[0, 0], oseq, fr) == [], (k_tie, dsts)
+
+
+@pytest.mark.parametrize('S,G', [(4, 4), (1, 4), (4, 2)], ids=['split_G4S4', 'fused', 'split_G2S4'])
+def test_decode_streams_do_not_change_results(eng, S, G):
+    """members split over 1..4 streams (nicnes_set_decode_streams; 7 members split unevenly, ragged
+    100-row slabs): fitness, tokens and log-probs bit-identical to the one-stream decode"""
+    dims = O.Dims()
+    _load(eng, O.make_theta(dims, 6, 4.0, 0.1), _fc(100, 77))
+    eng.set_decode_split(S, G)
+    out = {}
+    try:
+        for n in (1, 2, 3, 4):
+            eng.set_decode_streams(n)
+            fit, seq, lp = eng.evaluate(6, 2, 7, SIGMA, return_seq=True, return_lp=True)
+            out[n] = (fit.clone(), seq.clone(), lp.clone())
+    finally:
+        eng.set_decode_streams(0)
+        eng.set_decode_split(0, 0)
+    for n in (2, 3, 4):
+        for a, b in zip(out[1], out[n]):
+            assert torch.equal(a, b), n
