@@ -57,6 +57,12 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef MFMA_FIRST_SIGN
 #define MFMA_FIRST_SIGN 0  // logit stages: the sign whose waves run the stage's MFMAs before the previous epilogue
 #endif
+#ifndef LOGIT_MIDSTORE
+#define LOGIT_MIDSTORE 1   // logit stages: the next stage's W+- tile is stored among the MFMAs of this one
+#endif
+#ifndef LOGIT_MID_AT
+#define LOGIT_MID_AT 6     // ... before half-chunk LOGIT_MID_AT of 8 (measured: 5-7 equal, 2 and 8 -0.8 %)
+#endif
 #ifndef DECODE_PRIO
 #define DECODE_PRIO 0      // s_setprio 1 for one half of the workgroup's waves: 1 = waves 4-7, 2 = waves 0-3
 #endif
@@ -343,14 +349,29 @@ __device__ __forceinline__ void mfma_stage64(const float* w, const float* bias, 
     }
 }
 
+struct NoMid {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+// mid() runs before half-chunk MID of the 8 (8: after the last MFMA; 9: never): the logit loop's W+- store
+// of the next stage and the loads of the one after (LOGIT_MIDSTORE)
+template <int MID = 8, class Mid = NoMid>
 __device__ __forceinline__ void mfma_stage64_o(const float* w, const float* bias, const float (&Bop)[64], int arow,
-                                               int hh, f32x16& acc0, f32x16& acc1) {
+                                               int hh, f32x16& acc0, f32x16& acc1, Mid&& mid = Mid()) {
     const float* row0 = w + arow;
     const float* row1 = row0 + 32 * LDS_ROW;
     acc0 = bias_init(bias, hh);
     acc1 = bias_init(bias + 32, hh);
+    auto at = [&](int h) __attribute__((always_inline)) {   // mid() before half-chunk h (8 halves of 8 k pairs)
+        if (h == MID) {
+            __builtin_amdgcn_sched_barrier(0);
+            mid();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
 #pragma unroll
     for (int T = 0; T < 4; ++T) {
+        at(2 * T);
         f32x4 a0[4], a1[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -359,23 +380,38 @@ __device__ __forceinline__ void mfma_stage64_o(const float* w, const float* bias
         }
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) {
+            if (jj == 8) at(2 * T + 1);
             acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bop[16 * T + jj], acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
         }
     }
+    at(8);
 }
 
-__device__ __forceinline__ f32x16 mfma_tile_o(f32x16 acc, const float* w, const float (&Bop)[64], int arow) {
+template <int MID = 8, class Mid = NoMid>
+__device__ __forceinline__ f32x16 mfma_tile_o(f32x16 acc, const float* w, const float (&Bop)[64], int arow,
+                                              Mid&& mid = Mid()) {
     const float* row = w + arow;
+    auto at = [&](int h) __attribute__((always_inline)) {
+        if (h == MID) {
+            __builtin_amdgcn_sched_barrier(0);
+            mid();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
 #pragma unroll
     for (int T = 0; T < 4; ++T) {
+        at(2 * T);
         f32x4 a[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) a[c] = *reinterpret_cast<const f32x4*>(row + T * 32 + 4 * c);
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj)
+        for (int jj = 0; jj < 16; ++jj) {
+            if (jj == 8) at(2 * T + 1);
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[jj >> 2][jj & 3], Bop[16 * T + jj], acc, 0, 0, 0);
+        }
     }
+    at(8);
     return acc;
 }
 
@@ -673,21 +709,34 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
     Stage64Regs s64;
     stage64_load_o(lsrc(s0), lo, bias, s64);
     stage64_store_o(lds, lsrc(s0).valid, lo, bias, s64);
+#if LOGIT_MIDSTORE
+    // the registers carry stage s + 1 into stage s: its W+- tile is written before the last quarter of the
+    // MFMAs of stage s (its buffer was last read in stage s - 1), then the loads of stage s + 2 are issued,
+    // so the end of a stage has no staging wait and no LDS-write tail in front of the barrier
+    stage64_load_o(lsrc(min(s0 + 1, s1 - 1)), lo, bias, s64);
+#endif
     __syncthreads();
     f32x16 a0, a1, b0, b1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { b0[r] = NEG_INF; b1[r] = NEG_INF; }
     auto stage = [&](int s, f32x16& o0, f32x16& o1, const f32x16& q0, const f32x16& q1) {
         const int sn = min(s + 1, s1 - 1);
-#if !(DECODE_ABLATE & 2)
+#if !LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
         stage64_load_o(lsrc(sn), lo, bias, s64);
 #endif
         const float* buf = lds + ((s - s0) & 1) * STAGE64_FLOATS;
         const float* wsg = buf + sgn * (64 * LDS_ROW);
         const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * sgn;
+        auto mid = [&]() __attribute__((always_inline)) {
+#if LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
+            stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
+            stage64_load_o(lsrc(min(s + 2, s1 - 1)), lo, bias, s64);
+#endif
+        };
+        constexpr int MID = LOGIT_MIDSTORE ? LOGIT_MID_AT : 9;   // 9: never
         if constexpr (G == 4) {
             if (sgn == MFMA_FIRST_SIGN) {
-                mfma_stage64_o(wsg, bsg, hB, lo.arow, hh, o0, o1);
+                mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
 #if !(DECODE_ABLATE & 1)
                 epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
 #endif
@@ -695,20 +744,20 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
 #if !(DECODE_ABLATE & 1)
                 epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
 #endif
-                mfma_stage64_o(wsg, bsg, hB, lo.arow, hh, o0, o1);
+                mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
             }
         } else {
             const float* w1 = wsg + 32 * hf * LDS_ROW;         // this wave's 32-row tile of the stage
             const float* bb = bsg + 32 * hf;
             if (sgn == MFMA_FIRST_SIGN) {
-                o0 = mfma_tile_o(bias_init(bb, hh), w1, hB, lo.arow);
+                o0 = mfma_tile_o<MID>(bias_init(bb, hh), w1, hB, lo.arow, mid);
                 epilogue32<PAIRS>(st, q0, 64 * (s - 1) + vl);
             } else {
                 epilogue32<PAIRS>(st, q0, 64 * (s - 1) + vl);
-                o0 = mfma_tile_o(bias_init(bb, hh), w1, hB, lo.arow);
+                o0 = mfma_tile_o<MID>(bias_init(bb, hh), w1, hB, lo.arow, mid);
             }
         }
-#if !(DECODE_ABLATE & 2)
+#if !LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
         stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
 #endif
 #if !(DECODE_ABLATE & 8)
@@ -1021,7 +1070,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
     __syncthreads();
     f32x16 hold;
     // fold of gate tile m (s_ = its gate sums) into the unit block's c' / h'
-    auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) {
+    auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) __attribute__((always_inline)) {
         const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
         const int U = m / 5, j5 = m % 5;
         if (j5 == 0) {                                           // g1
@@ -1046,7 +1095,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
                 st1(c.scr_r, lo_, H_SLOT(16 * U + r), CELL_SIG(s_[r]) * CELL_TANH(hold[r]));
         }
     };
-    auto load_c = [&](int m) {                                   // c of the f tile's unit block
+    auto load_c = [&](int m) __attribute__((always_inline)) {                                   // c of the f tile's unit block
         f32x16 cp;
         const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
 #pragma unroll
@@ -1064,7 +1113,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
             mfma_xh_part<0, 4, false>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
         else
             mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
-        fold(m, a0 + a1, cpre);                                  // i2h(x) + h2h(h), nets.py:109-111
+        fold(m, a0 + a1, cpre);                            // i2h(x) + h2h(h), nets.py:109-111
         if (m < 19) stage64_store(lds + ((m + 1 + b0) & 1) * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
         __syncthreads();
         PROF_MARK(120 + 24 * (t + 1) + 2 + m);
@@ -1326,7 +1375,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
     __syncthreads();
     PROF_SPLIT(pb0 + 2);
     f32x16 hold;
-    auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) {
+    auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) __attribute__((always_inline)) {
         const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
         const int U = m / 5, j5 = m % 5;
         if (j5 == 0) {                                           // g1
@@ -1351,7 +1400,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
                 st1(c.scr_r, lo_, HP_SLOT(hpar, 16 * U + r), CELL_SIG(s_[r]) * CELL_TANH(hold[r]));
         }
     };
-    auto load_c = [&](int m) {                                   // c of the f tile's unit block
+    auto load_c = [&](int m) __attribute__((always_inline)) {                                   // c of the f tile's unit block
         f32x16 cp;
         const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
 #pragma unroll
