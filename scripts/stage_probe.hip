@@ -156,6 +156,83 @@ void run(const char* name, const float* w, const float* z, float* out) {
            flops / best / 1e9 / 157.3 * 100.0 / 1000.0, best * 1e3 / nst);
 }
 
+
+// sign-split layout: a 4-wave workgroup per (member, sign), two per CU; each stages its own sign's 64-row
+// tile (W0 + z loaded per workgroup, so every element is loaded twice per CU, written once per sign)
+__global__ __launch_bounds__(256) void stage_probe_split(const float* __restrict__ w, const float* __restrict__ z,
+                                                         float* out, int nst, float sigma) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const float sg = (blockIdx.x & 1) ? -sigma : sigma;
+    float hB[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) hB[i] = 1e-3f * (float)((lane + i) & 7);
+    for (int i = tid; i < 2 * (64 * LDS_ROW + 64); i += 256) lds[i] = 1e-3f * (float)(i & 15);
+    __syncthreads();
+    f32x16 acc0 = {}, acc1 = {};
+    f32x4 sw[8], sz[8];
+    const size_t so = (size_t)(blockIdx.x >> 1) * 65536 + 4 * tid;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { sw[u] = *(const f32x4*)(w + so + 1024 * u); sz[u] = *(const f32x4*)(z + so + 1024 * u); }
+    const int arow = (lane & 31) * LDS_ROW + 16 * (lane >> 5);
+    for (int s = 0; s < nst; ++s) {
+        const float* buf = lds + (s & 1) * (64 * LDS_ROW + 64);
+        f32x4 nw[8], nz[8];
+        const size_t o2 = so + (size_t)((s + 1) & 15) * 8192;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { nw[u] = *(const f32x4*)(w + o2 + 1024 * u); nz[u] = *(const f32x4*)(z + o2 + 1024 * u); }
+#pragma unroll
+        for (int T = 0; T < 4; ++T) {
+            f32x4 a0[4], a1[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                a0[c] = *reinterpret_cast<const f32x4*>(buf + arow + T * 32 + 4 * c);
+                a1[c] = *reinterpret_cast<const f32x4*>(buf + 32 * LDS_ROW + arow + T * 32 + 4 * c);
+            }
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], hB[16 * T + jj], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], hB[16 * T + jj], acc1, 0, 0, 0);
+            }
+        }
+        float* b = lds + ((s + 1) & 1) * (64 * LDS_ROW + 64) + (tid >> 5) * LDS_ROW + 4 * (tid & 31);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            *reinterpret_cast<f32x4*>(b + 8 * u * LDS_ROW) = sw[u] + sg * sz[u];
+            sw[u] = nw[u];
+            sz[u] = nz[u];
+        }
+        __syncthreads();
+    }
+    float r = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r += acc0[i] + acc1[i];
+    out[blockIdx.x * 256 + tid] = r;
+}
+
+void run_split(const char* name, const float* w, const float* z, float* out) {
+    const int nst = 150, blocks = 512;
+    const size_t lds = 2 * (64 * LDS_ROW + 64) * sizeof(float);
+    hipFuncSetAttribute((const void*)stage_probe_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipLaunchKernelGGL(stage_probe_split, dim3(blocks), dim3(256), lds, 0, w, z, out, 10, 0.01f);
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; ++rep) {
+        hipEventRecord(e0);
+        hipLaunchKernelGGL(stage_probe_split, dim3(blocks), dim3(256), lds, 0, w, z, out, nst, 0.01f);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        best = ms < best ? ms : best;
+    }
+    const double flops = (double)blocks * 4 * nst * 128 * 32 * 32 * 2 * 2;
+    printf("%-40s %8.3f ms  %7.1f TFLOP/s  %5.1f%% of 157.3  %6.2f us/stage\n", name, best, flops / best / 1e9,
+           flops / best / 1e9 / 157.3 * 100.0 / 1000.0, best * 1e3 / nst);
+}
+
 int main() {
     float *w, *z, *out;
     const size_t n = (size_t)256 * 65536 + 16 * 8192 + 8192;
@@ -173,5 +250,7 @@ int main() {
     run<true, true, 4>("  staging: VALU only", w, z, out);
     run<true, true, 5>("W+- staging, loads spread over the MFMAs", w, z, out);
     run<true, true, 6>("W+- staging by the sign-0 waves only", w, z, out);
+    run_split("sign-split: 2 x 4-wave workgroups per CU", w, z, out);
+    run<true, true, 1>("A from LDS, barrier, W+- staging (again)", w, z, out);
     return 0;
 }
