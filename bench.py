@@ -290,6 +290,7 @@ def main():
                                 'cell_ms': round(ph['cell_ms'], 3),
                                 'shape': {'row_groups': G, 'slabs': nslabs, 'logit_split': S_split}}},
         'cpu_baseline': cpu,
+        'decodes_per_s': round(2 * value, 3),        # one decode = one sign's rollout of the batch
         'tie_fallbacks': eng.stats()['tie_fallbacks'],
         'update_ratio': ratio,
     }
