@@ -72,7 +72,8 @@ def iteration_algorithmic_bytes(B, P, D=2865808):
     return P * (step_noise_bytes_per_member(B) + 4 * D) + 4 * D + (3 * 2 * 8 + 4 + 4) * D
 
 
-PMC_FILES = {('nicnes_decode_step_kernel', 512, 128): 'profiles/r02_pmc_step_p512_b128.json',
+PMC_FILES = {('nicnes_decode_steps_kernel', 512, 128): 'profiles/r02_pmc_steps_p512_b128.json',
+             ('nicnes_decode_step_kernel', 512, 128): 'profiles/r02_pmc_step_p512_b128.json',
              ('nicnes_decode_logit_kernel<4>', 64, 128): 'profiles/r02_pmc_logit_p64_b128.json'}
 
 
@@ -217,9 +218,9 @@ def main():
     value = P * args.steps / dt
     dec_s = float(np.mean(dec_ms)) / 1e3
     flops = decode_flops_per_member(B) * P_local
-    # dominant kernel: the fused step kernel (logits + token + next LSTM cell, T + 2 launches per
-    # evaluate) or, on the split path (members x slabs below the CU count), the logit kernel (T
-    # launches); per-launch figures are the evaluate's totals / launches (what rocprofv3 --stats
+    # dominant kernel: the fused steps kernel (logits + token + next LSTM cell for every step t = -1..T,
+    # one launch per evaluate) or, on the split path (members x slabs below the CU count), the logit kernel
+    # (T launches); per-launch figures are the evaluate's totals / launches (what rocprofv3 --stats
     # averages over the same launches)
     ph = phases[-1]
     G, nslabs, S_split = eng.decode_shape(B, P_local)
@@ -231,7 +232,10 @@ def main():
         step_flop = flops
         alg_bytes = step_noise_bytes_per_member(B) * P_local
     elif ph['step_launches']:
-        kname, n_step = 'nicnes_decode_step_kernel', ph['step_launches']
+        # fused path: every step of a workgroup in one launch (nicnes_decode_steps_kernel), or one launch
+        # per step t = -1..T (nicnes_decode_step_kernel, DECODE_PERSISTENT=0 builds)
+        kname = 'nicnes_decode_steps_kernel' if ph['step_launches'] == 1 else 'nicnes_decode_step_kernel'
+        n_step = ph['step_launches']
         step_ms = float(np.mean([q['step_ms'] for q in phases])) / n_step
         step_flop = step_flops_per_member(B) * P_local / n_step
         alg_bytes = step_noise_bytes_per_member(B) * P_local / n_step

@@ -32,6 +32,7 @@ struct DecodeParams {
 // launch kinds recorded next to the timing events
 #define DK_IMG 0
 #define DK_STEP 1        // fused step kernel (logits of t + cell of t + 1)
+#define DK_STEPS 4       // fused path, every step in one launch (nicnes_decode_steps_kernel)
 #define DK_CELL 2        // split path: token merge of t + cell of t + 1
 #define DK_LOGIT 3       // split path: logits of t over one vocabulary range
 

@@ -57,6 +57,9 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef MFMA_FIRST_SIGN
 #define MFMA_FIRST_SIGN 0  // logit stages: the sign whose waves run the stage's MFMAs before the previous epilogue
 #endif
+#ifndef DECODE_PERSISTENT
+#define DECODE_PERSISTENT 1  // fused path: every step of a workgroup in one launch (0: one launch per step)
+#endif
 #ifndef LOGIT_MIDSTORE
 #define LOGIT_MIDSTORE 1   // logit stages: the next stage's W+- tile is stored among the MFMAs of this one
 #endif
@@ -930,12 +933,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
 // go to lane scratch. In the logit loop the two waves sharing a SIMD (w and w+4: opposite signs)
 // run the MFMA chains and the VALU epilogue of the previous stage in opposite orders, so VALU of
 // one wave overlaps the MFMAs of the other.
+// one step of one workgroup; false when the workgroup is done (every row finished, or t = T)
 template <bool PAIRS>
-__global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodeParams p, int t) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const Ctx c = make_ctx(p);
-    if (t > 0 && p.alive[c.wg] == 0) return;
-    wave_prio(c.wave);
+__device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, float* lds, int t) {
     PROF_MARK(2 * (t + 1));
     const uint32_t lo = 4u * c.lane;
     const int nst = (p.V1 + 63) >> 6;
@@ -1026,9 +1026,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
 #endif
         const int any = __syncthreads_or(((unfinished && c.row_valid) || (DECODE_ABLATE & 64)) ? 1 : 0);
         if (c.tid == 0) p.alive[c.wg] = any;
-        if (!any) { PROF_MARK(2 * (t + 1) + 1); return; }       // the reference stops here (nets.py:242-243)
+        if (!any) { PROF_MARK(2 * (t + 1) + 1); return false; } // the reference stops here (nets.py:242-243)
     }
-    if (t >= p.T) { PROF_MARK(2 * (t + 1) + 1); return; }
+    if (t >= p.T) { PROF_MARK(2 * (t + 1) + 1); return false; }
 
     // ---- LSTM cell of step t+1 ---------------------------------------------------------------
     float xB[64];
@@ -1119,6 +1119,31 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
         PROF_MARK(120 + 24 * (t + 1) + 2 + m);
     }
     PROF_MARK(2 * (t + 1) + 1);
+    return true;
+}
+
+template <bool PAIRS>
+__global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodeParams p, int t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const Ctx c = make_ctx(p);
+    if (t > 0 && p.alive[c.wg] == 0) return;
+    wave_prio(c.wave);
+    step_body<PAIRS>(p, c, lds, t);
+}
+
+// The whole decode of a workgroup (steps t = -1 .. T) in one launch: a member's steps depend only on
+// that member, so nothing needs a grid-wide step boundary. Saves the per-launch ramp and tail (every
+// CU waits for the slowest at each of the T + 2 step boundaries), the launch gaps and the per-launch
+// workgroup setup; the state between steps stays in the same lane scratch, and a lane re-reads only
+// slots it wrote itself (a same-address store -> load of one lane: ordered like any C++ store/load pair).
+// The LDS stage buffers are free at a step boundary: every step ends on a barrier after its last read.
+template <bool PAIRS>
+__global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodeParams p) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const Ctx c = make_ctx(p);
+    wave_prio(c.wave);
+    for (int t = -1; t <= p.T; ++t)
+        if (!step_body<PAIRS>(p, c, lds, t)) break;
 }
 
 // ========== split path: one member step over several workgroups =================================
@@ -1462,6 +1487,8 @@ extern "C" hipError_t nicnes_decode_init() {
     const struct { const void* f; size_t b; } ks[] = {
         {(const void*)nicnes_decode_step_kernel<true>, LDS64},
         {(const void*)nicnes_decode_step_kernel<false>, LDS64},
+        {(const void*)nicnes_decode_steps_kernel<true>, LDS64},
+        {(const void*)nicnes_decode_steps_kernel<false>, LDS64},
         {(const void*)nicnes_decode_logit_kernel<4, true>, LDS64},
         {(const void*)nicnes_decode_logit_kernel<4, false>, LDS64},
         {(const void*)nicnes_decode_logit_kernel<2, true>, LDS64},
@@ -1514,12 +1541,20 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
         hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(1, member_count, nslabs), block, LDS32, stream, *p);
         mark(DK_IMG);
         const dim3 grid(member_count, nslabs);
-        for (int t = -1; t <= p->T; ++t) {
+        if (DECODE_PERSISTENT && !DECODE_PROF) {
             if (pairs)
-                hipLaunchKernelGGL(nicnes_decode_step_kernel<true>, grid, block, LDS64, stream, *p, t);
+                hipLaunchKernelGGL(nicnes_decode_steps_kernel<true>, grid, block, LDS64, stream, *p);
             else
-                hipLaunchKernelGGL(nicnes_decode_step_kernel<false>, grid, block, LDS64, stream, *p, t);
-            mark(DK_STEP);
+                hipLaunchKernelGGL(nicnes_decode_steps_kernel<false>, grid, block, LDS64, stream, *p);
+            mark(DK_STEPS);
+        } else {
+            for (int t = -1; t <= p->T; ++t) {
+                if (pairs)
+                    hipLaunchKernelGGL(nicnes_decode_step_kernel<true>, grid, block, LDS64, stream, *p, t);
+                else
+                    hipLaunchKernelGGL(nicnes_decode_step_kernel<false>, grid, block, LDS64, stream, *p, t);
+                mark(DK_STEP);
+            }
         }
     } else {
         const int Sc = p->S < 4 ? p->S : 4;

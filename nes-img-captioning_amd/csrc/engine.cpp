@@ -906,8 +906,8 @@ int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host) {
     if (h->n_dev < 3) return NICNES_ERR_INVALID;
     HIPC(h, hipSetDevice(h->device));
     HIPC(h, hipEventSynchronize(h->dev[h->n_dev - 1]));
-    // event k follows launch k. Fused: img, then step(t) for t = -1..T (the first two launches run
-    // only a cell). Split: img, cell(-1), cell(0), then logit(t), cell(t) for t = 1..T.
+    // event k follows launch k. Fused: img, then steps (one launch), or step(t) for t = -1..T (the first
+    // two launches run only a cell). Split: img, cell(-1), cell(0), then logit(t), cell(t) for t = 1..T.
     float o[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ms = 0.f;
     int n_cell_only = 0;
     for (int k = 1; k < h->n_dev; ++k) {
@@ -918,6 +918,7 @@ int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host) {
                 o[2] += ms; o[3] += 1;
                 if (n_cell_only < 2) { o[1] += ms; ++n_cell_only; }
                 break;
+            case DK_STEPS: o[2] += ms; o[3] += 1; break;      // every step in one launch
             case DK_LOGIT: o[4] += ms; o[5] += 1; break;
             default:
                 o[6] += ms; o[7] += 1;

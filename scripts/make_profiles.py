@@ -20,7 +20,7 @@ rnd = sys.argv[2] if len(sys.argv) > 2 else 'r02'
 src = os.path.join(REPO, 'gpurun_out', tag)
 out = os.path.join(REPO, 'profiles')
 B = 128
-for P, key, kernel in ((512, 'step', 'nicnes_decode_step_kernel'), (64, 'logit', 'nicnes_decode_logit_kernel')):
+for P, key, kernel in ((512, 'steps', 'nicnes_decode_steps_kernel'), (64, 'logit', 'nicnes_decode_logit_kernel')):
     st = os.path.join(src, 'stats%d' % P)
     shutil.copy(os.path.join(st, 'run_kernel_stats.csv'), os.path.join(out, '%s_kernel_stats_p%d.csv' % (rnd, P)))
     launches = os.path.join(out, '%s_decode_launches_p%d.json' % (rnd, P))
@@ -31,8 +31,8 @@ for P, key, kernel in ((512, 'step', 'nicnes_decode_step_kernel'), (64, 'logit',
         lj = json.load(f)
     rec = [v for k, v in lj['kernels'].items() if kernel in k][0]
     dur_ms = rec['mean_ms_full_grid']
-    if key == 'step':
-        n_launch = 18
+    if key in ('step', 'steps'):
+        n_launch = 18 if key == 'step' else 1           # one launch per step, or every step in one launch
         flop = bench.step_flops_per_member(B) * P / n_launch
         alg = bench.step_noise_bytes_per_member(B) * P / n_launch
     else:
