@@ -57,9 +57,6 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef MFMA_FIRST_SIGN
 #define MFMA_FIRST_SIGN 0  // logit stages: the sign whose waves run the stage's MFMAs before the previous epilogue
 #endif
-#ifndef SCALAR_WPLUS
-#define SCALAR_WPLUS 0
-#endif
 #ifndef DECODE_PERSISTENT
 #define DECODE_PERSISTENT 1  // fused path: every step of a workgroup in one launch (0: one launch per step)
 #endif
@@ -315,25 +312,13 @@ __device__ __forceinline__ void stage64_load_o(const StageSrc& S, const LaneOffs
     }
 }
 
-// W+ = w + delta as four v_add_f32 (a plain f32x4 '+' becomes two v_pk_add_f32)
-__device__ __forceinline__ f32x4 add4s(f32x4 a, f32x4 b) {
-#if SCALAR_WPLUS
-    f32x4 r;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) asm("v_add_f32 %0, %1, %2" : "=v"(r[e]) : "v"(a[e]), "v"(b[e]));
-    return r;
-#else
-    return a + b;
-#endif
-}
-
 __device__ __forceinline__ void stage64_store_o(float* buf, int valid, const LaneOffs& o, bool bias,
                                                 const Stage64Regs& r) {
     float* b = buf + o.so;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const f32x4 delta = r.z[u];                   // fp32(sigma * z) from the sigma-scaled table, nets.py:102
-        *reinterpret_cast<f32x4*>(b + 16 * u * LDS_ROW) = add4s(r.w[u], delta);            // nets.py:113
+        *reinterpret_cast<f32x4*>(b + 16 * u * LDS_ROW) = r.w[u] + delta;                  // nets.py:113
         *reinterpret_cast<f32x4*>(b + (64 + 16 * u) * LDS_ROW) = r.w[u] - delta;           // nic_nes_worker.py:151
     }
     if (bias) {
