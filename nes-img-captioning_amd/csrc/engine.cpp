@@ -903,7 +903,7 @@ int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host) {
         for (int i = 0; i < 8; ++i) out8_host[i] = 0.f;
         return NICNES_OK;
     }
-    if (h->n_dev < 3) return NICNES_ERR_INVALID;
+    if (h->n_dev < 2) return NICNES_ERR_INVALID;
     HIPC(h, hipSetDevice(h->device));
     HIPC(h, hipEventSynchronize(h->dev[h->n_dev - 1]));
     // event k follows launch k. Fused: img, then steps (one launch), or step(t) for t = -1..T (the first
