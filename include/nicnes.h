@@ -210,17 +210,17 @@ int nicnes_set_timing(nicnes_handle* h, int on);
 int nicnes_kernel_times(nicnes_handle* h, float* out2_host);
 
 /* Per-kernel split of the last timed decode (events between its launches), in ms: [0] img-embed
- * kernel, [1] the two cell-only launches (t = -1, 0), [2] fused step launches summed (logits + token
- * + next cell, t = -1..T), [3] their count, [4] split-path logit launches summed, [5] their count,
- * [6] split-path cell launches summed (token merge + next cell, t = -1..T), [7] their count.
- * Synchronising. */
+ * kernel, [1] the two cell-only launches (t = -1, 0; one-launch-per-step builds only), [2] fused
+ * path: the steps kernel (every step t = -1..T in one launch; or the per-step launches summed),
+ * [3] its launch count, [4] split-path logit launches summed, [5] their count, [6] split-path cell
+ * launches summed (token merge + next cell, t = -1..T), [7] their count. Synchronising. */
 int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host);
 
 /* Decode launch shape. Not a reference interface: the reference decodes one member per CPU process
  * (src/algorithm/nic_nes/nic_nes_worker.py:142-154); the engine spreads a member over S workgroups
  * when members x slabs cannot fill the GPU. S = 0 / G = 0 pick automatically (S from the CU count,
  * G = 2 -- 64-row slabs -- when B pads to fewer rows that way, e.g. mscoco_nes.json batch_size 64).
- * G = 4 with S = 1 is the fused one-launch-per-step kernel. Tokens do not depend on the shape. */
+ * G = 4 with S = 1 is the fused path (one launch for every step). Tokens do not depend on the shape. */
 int nicnes_set_decode_split(nicnes_handle* h, int32_t S, int32_t G);
 /* the shape an evaluate of `count` members of a B-image batch would use: [0] G, [1] slabs, [2] S */
 int nicnes_decode_shape(nicnes_handle* h, int32_t B, int32_t count, int32_t* out3_host);
