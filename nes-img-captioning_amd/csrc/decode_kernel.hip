@@ -60,6 +60,9 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef DECODE_PERSISTENT
 #define DECODE_PERSISTENT 1  // fused path: every step of a workgroup in one launch (0: one launch per step)
 #endif
+#ifndef IMG64
+#define IMG64 1            // fused path: image projection in 64-row stages with the fc chunk in registers
+#endif
 #ifndef LOGIT_MIDSTORE
 #define LOGIT_MIDSTORE 1   // logit stages: the next stage's W+- tile is stored among the MFMAs of this one
 #endif
@@ -922,6 +925,104 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
     if (fused_path) PROF_MARK(81); else PROF_SPLIT(251);
 }
 
+// ========== t = 0 input on the fused path: 64-row stages, fc chunk as a register B operand ==========
+// x = img_embed(fc) of both signs for the workgroup's 128 rows (nets.py:194-195): 2 nK stages of 64 img_w rows
+// (unit blocks 0-1 for even stages, 2-3 for odd) x 128 k (chunk j >> 1), staged and double-buffered as the logit
+// stages; the fc chunk of the lane's row (64 values) is the B operand of both stages of a chunk, the next chunk's
+// loaded during the current one. Every unit-block chain starts from the bias and takes k in the same order as
+// nicnes_decode_img_kernel: identical x, written to X_SLOT.
+__global__ __launch_bounds__(NTHREADS) void nicnes_decode_img64_kernel(DecodeParams p) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const Ctx c = make_ctx(p);
+    PROF_MARK(80);
+    const float* fcm = p.fc + (p.member_batch ? (size_t)p.member_batch[c.member] * p.B * p.F : 0);
+    const rsrc_t fc_r = make_rsrc(fcm, 4u * (uint32_t)p.B * (uint32_t)p.F);
+    const int nK = p.F >> 7;
+    const uint32_t F = (uint32_t)p.F;
+    auto load = [&](int j, Stage64Regs& r) __attribute__((always_inline)) {
+        const int tid = c.wave * 64 + lane_fresh();
+        // thread tid: img_w row 64 (j & 1) + (tid >> 5) + 16 u, k 128 (j >> 1) + 4 (tid & 31) (stage64_store's rows)
+        const uint32_t vo = 4u * ((uint32_t)(tid >> 5) * F + 4u * (uint32_t)(tid & 31));
+        const uint32_t base = 4u * ((uint32_t)p.off_img_w + (uint32_t)(64 * (j & 1)) * F + 128u * (uint32_t)(j >> 1));
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            r.w[u] = ld4(c.theta_r, vo, base + 64u * F * (uint32_t)u);
+            r.z[u] = ld4(c.noise_r, vo, base + 64u * F * (uint32_t)u);
+        }
+        const uint32_t bo = 4u * ((uint32_t)p.off_img_b + (uint32_t)(64 * (j & 1) + (tid & 63)));
+        r.bw = ld1(c.theta_r, bo);
+        r.bz = ld1(c.noise_r, bo);
+    };
+    auto load_fc = [&](int kc, float (&dst)[64]) __attribute__((always_inline)) {
+        const uint32_t frow = 4u * ((uint32_t)c.bc * F + 128u * (uint32_t)kc + 4u * (uint32_t)c.hh);
+#pragma unroll
+        for (int T = 0; T < 4; ++T)
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const f32x4 v = ld4(fc_r, frow + 4u * (uint32_t)(32 * T + 8 * a));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) dst[16 * T + 4 * a + e] = v[e];
+            }
+    };
+    // two chains (unit blocks u0, u0 + 1) over one stage, accumulating (bias first at chunk 0)
+    auto mm = [&](const float* buf, bool first, const float (&Bop)[64], f32x16& A0, f32x16& A1)
+        __attribute__((always_inline)) {
+        const int lane = lane_fresh(), hh = lane >> 5;
+        const float* wsg = buf + c.sgn * (64 * LDS_ROW);
+        const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * c.sgn;
+        if (first) {
+            A0 = bias_init(bsg, hh);
+            A1 = bias_init(bsg + 32, hh);
+        }
+        const float* row0 = wsg + (lane & 31) * LDS_ROW + 16 * hh;
+        const float* row1 = row0 + 32 * LDS_ROW;
+#pragma unroll
+        for (int T = 0; T < 4; ++T) {
+            f32x4 a0[4], a1[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                a0[q] = *reinterpret_cast<const f32x4*>(row0 + T * 32 + 4 * q);
+                a1[q] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * q);
+            }
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+                A0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bop[16 * T + jj], A0, 0, 0, 0);
+                A1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], A1, 0, 0, 0);
+            }
+        }
+    };
+    const int tid0 = c.wave * 64;
+    Stage64Regs s64;
+    f32x16 acc[4];
+    float fcB[64], fcN[64];
+    load(0, s64);
+    load_fc(0, fcB);
+    stage64_store(lds, 64, tid0 + lane_fresh(), s64);
+    __syncthreads();
+#pragma unroll 1
+    for (int kc = 0; kc < nK; ++kc) {
+        load(2 * kc + 1, s64);                                   // stage 2 kc + 1: unit blocks 2-3
+        if (kc + 1 < nK) load_fc(kc + 1, fcN);
+        mm(lds, kc == 0, fcB, acc[0], acc[1]);
+        stage64_store(lds + STAGE64_FLOATS, 64, tid0 + lane_fresh(), s64);
+        __syncthreads();
+        if (kc + 1 < nK) load(2 * kc + 2, s64);                  // stage 2 kc + 2: unit blocks 0-1
+        mm(lds + STAGE64_FLOATS, kc == 0, fcB, acc[2], acc[3]);
+        if (kc + 1 < nK) stage64_store(lds, 64, tid0 + lane_fresh(), s64);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 64; ++i) fcB[i] = fcN[i];
+    }
+    const uint32_t lo = 4u * (uint32_t)lane_fresh();
+#pragma unroll
+    for (int U = 0; U < 4; ++U)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st1(c.scr_r, lo, X_SLOT(16 * U + r), acc[U][r]);
+    st1(c.scr_r, lo, U_SLOT, 1.0f);
+    if (c.tid == 0) p.alive[c.wg] = 1;
+    PROF_MARK(81);
+}
+
 // ========== step kernel: logits + greedy token of step t, then the LSTM cell of step t+1 ========
 // One launch per step t = -1 .. T. Logits (nets.py:202,208-209) run for t >= 1 over h = h_t (t = 0
 // is the image step, whose output the reference discards). The cell of step t+1 (nets.py:98-134)
@@ -1487,6 +1588,7 @@ extern "C" hipError_t nicnes_decode_init() {
     const struct { const void* f; size_t b; } ks[] = {
         {(const void*)nicnes_decode_step_kernel<true>, LDS64},
         {(const void*)nicnes_decode_step_kernel<false>, LDS64},
+        {(const void*)nicnes_decode_img64_kernel, LDS64},
         {(const void*)nicnes_decode_steps_kernel<true>, LDS64},
         {(const void*)nicnes_decode_steps_kernel<false>, LDS64},
         {(const void*)nicnes_decode_logit_kernel<4, true>, LDS64},
@@ -1538,7 +1640,10 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
     const bool pairs = p->bounded_lse && p->lp == nullptr;
     mark(0);
     if (fused) {
-        hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(1, member_count, nslabs), block, LDS32, stream, *p);
+        if (IMG64)
+            hipLaunchKernelGGL(nicnes_decode_img64_kernel, dim3(member_count, nslabs), block, LDS64, stream, *p);
+        else
+            hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(1, member_count, nslabs), block, LDS32, stream, *p);
         mark(DK_IMG);
         const dim3 grid(member_count, nslabs);
         if (DECODE_PERSISTENT && !DECODE_PROF) {
