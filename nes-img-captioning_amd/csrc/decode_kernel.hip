@@ -63,6 +63,9 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef IMG64
 #define IMG64 1            // fused path: image projection in 64-row stages with the fc chunk in registers
 #endif
+#ifndef CROSS_PREFETCH
+#define CROSS_PREFETCH 1   // steps kernel: a phase's first staging tile loaded during the previous phase's last stage
+#endif
 #ifndef LOGIT_MIDSTORE
 #define LOGIT_MIDSTORE 1   // logit stages: the next stage's W+- tile is stored among the MFMAs of this one
 #endif
@@ -694,9 +697,30 @@ __device__ __forceinline__ void epilogue32(RowState& st, const f32x16& P0, int v
 // Stages alternate between two accumulator sets, so no stage copies its result for the next one's
 // epilogue; the two waves of a SIMD (w, w + 4: opposite signs) run MFMA and epilogue in opposite
 // orders. On return the last stage_store went to buffer (s1 - s0) & 1 (a redundant copy).
-template <int G, bool PAIRS>
+struct NoTail {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+// s64 carries staging registers in and out: with `preloaded` it already holds stage s0's loads (issued by
+// the caller, e.g. during the previous cell's last stage); tail() runs at the last stage's mid-point in place
+// of a store/load (the caller loads its next tile into s64 there)
+// where logit rows 64s .. 64s+63 of the member (noise slice at nidx) come from
+__device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t nidx, int s) {
+    StageSrc Sx;
+    Sx.w_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
+    Sx.z_r = make_rsrc(p.noise + nidx + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
+    Sx.b_r = make_rsrc(p.theta + p.off_log_b, 4u * (uint32_t)p.V1);
+    Sx.bz_r = make_rsrc(p.noise + nidx + p.off_log_b, 4u * (uint32_t)p.V1);
+    Sx.so_a = 32768u * (uint32_t)s; Sx.so_b = Sx.so_a + 16384u;
+    Sx.bso = 256u * (uint32_t)s; Sx.bda = 0u; Sx.bdb = 128u;
+    Sx.valid = p.V1 - 64 * s;
+    return Sx;
+}
+
+template <int G, bool PAIRS, class Tail = NoTail>
 __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, uint64_t nidx, int wave, int sgn,
-                                             int hf, const float (&hB)[64], int s0, int s1, RowState& st) {
+                                             int hf, const float (&hB)[64], int s0, int s1, RowState& st,
+                                             Stage64Regs& s64, bool preloaded = false, Tail&& tail = Tail()) {
     const rsrc_t lw_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
     const rsrc_t lz_r = make_rsrc(p.noise + nidx + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
     const rsrc_t lbw_r = make_rsrc(p.theta + p.off_log_b, 4u * (uint32_t)p.V1);
@@ -712,14 +736,13 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
     const LaneOffs lo = lane_offs(wave, 128u);
     const int hh = lane_fresh() >> 5, vl = 4 * hh + (G == 4 ? 0 : 32 * hf);
     const bool bias = wave < 2;
-    Stage64Regs s64;
-    stage64_load_o(lsrc(s0), lo, bias, s64);
+    if (!preloaded) stage64_load_o(lsrc(s0), lo, bias, s64);
     stage64_store_o(lds, lsrc(s0).valid, lo, bias, s64);
 #if LOGIT_MIDSTORE
     // the registers carry stage s + 1 into stage s: its W+- tile is written before the last quarter of the
     // MFMAs of stage s (its buffer was last read in stage s - 1), then the loads of stage s + 2 are issued,
     // so the end of a stage has no staging wait and no LDS-write tail in front of the barrier
-    stage64_load_o(lsrc(min(s0 + 1, s1 - 1)), lo, bias, s64);
+    if (s0 + 1 < s1) stage64_load_o(lsrc(s0 + 1), lo, bias, s64);
 #endif
     __syncthreads();
     f32x16 a0, a1, b0, b1;
@@ -735,8 +758,12 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
         const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * sgn;
         auto mid = [&]() __attribute__((always_inline)) {
 #if LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
-            stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
-            stage64_load_o(lsrc(min(s + 2, s1 - 1)), lo, bias, s64);
+            if (s + 1 < s1) {
+                stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
+                if (s + 2 < s1) stage64_load_o(lsrc(s + 2), lo, bias, s64);
+            } else {
+                tail();
+            }
 #endif
         };
         constexpr int MID = LOGIT_MIDSTORE ? LOGIT_MID_AT : 9;   // 9: never
@@ -1034,9 +1061,12 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img64_kernel(DecodePar
 // go to lane scratch. In the logit loop the two waves sharing a SIMD (w and w+4: opposite signs)
 // run the MFMA chains and the VALU epilogue of the previous stage in opposite orders, so VALU of
 // one wave overlaps the MFMAs of the other.
-// one step of one workgroup; false when the workgroup is done (every row finished, or t = T)
-template <bool PAIRS>
-__device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, float* lds, int t) {
+// one step of one workgroup; false when the workgroup is done (every row finished, or t = T).
+// s64 / pre (the steps kernel): staging registers kept across steps; pre says they hold this step's first
+// logit tile, loaded during the previous step's last cell stage (PREFETCH: that load is issued)
+template <bool PAIRS, bool PREFETCH>
+__device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, float* lds, int t, Stage64Regs& s64,
+                                          bool& pre) {
     PROF_MARK(2 * (t + 1));
     const uint32_t lo = 4u * c.lane;
     const int nst = (p.V1 + 63) >> 6;
@@ -1052,12 +1082,30 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
     }
 #pragma unroll
     for (int i = 0; i < 64; ++i) pin(hB[i]);
-    Stage64Regs s64;
+    const uint32_t ib = (uint32_t)p.off_i2h_b, hb = (uint32_t)p.off_h2h_b, bmin = min(ib, hb);
+    auto csrc = [&](int m) {                                     // gate tile m: i2h rows | h2h rows
+        const uint32_t r = gate_row(m);
+        StageSrc S;
+        S.w_r = c.theta_r; S.z_r = c.noise_r; S.b_r = c.theta_r; S.bz_r = c.noise_r;
+        S.so_a = 4u * ((uint32_t)p.off_i2h_w + 128u * r);
+        S.so_b = 4u * ((uint32_t)p.off_h2h_w + 128u * r);
+        S.bso = 4u * (bmin + r);
+        S.bda = 4u * (ib - bmin); S.bdb = 4u * (hb - bmin);
+        S.valid = 64;
+        return S;
+    };
     int it = 0;                                   // token fed to the next cell (0 = BOS at t = 0)
+    bool cell_pre = false;                        // s64 holds the cell's first gate tile
     if (nl > 0) {
         RowState st;
         row_state_init(st);
-        logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st);
+        // the cell's first gate tile does not depend on the token: its loads are issued at the last logit
+        // stage's mid-point (tail) and land while the token is picked
+        auto tail = [&]() __attribute__((always_inline)) {
+            if (CROSS_PREFETCH && t < p.T) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
+        };
+        logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail);
+        cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && t < p.T;
         PROF_MARK(120 + 24 * (t + 1));
 
         // ---- greedy token (nets.py:208-209) ------------------------------------------------
@@ -1152,21 +1200,9 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
     }
 #pragma unroll
     for (int i = 0; i < 64; ++i) pin(xB[i]);
-    const uint32_t ib = (uint32_t)p.off_i2h_b, hb = (uint32_t)p.off_h2h_b, bmin = min(ib, hb);
-    auto csrc = [&](int m) {                                     // gate tile m: i2h rows | h2h rows
-        const uint32_t r = gate_row(m);
-        StageSrc S;
-        S.w_r = c.theta_r; S.z_r = c.noise_r; S.b_r = c.theta_r; S.bz_r = c.noise_r;
-        S.so_a = 4u * ((uint32_t)p.off_i2h_w + 128u * r);
-        S.so_b = 4u * ((uint32_t)p.off_h2h_w + 128u * r);
-        S.bso = 4u * (bmin + r);
-        S.bda = 4u * (ib - bmin); S.bdb = 4u * (hb - bmin);
-        S.valid = 64;
-        return S;
-    };
     const int b0 = nl & 1;                                       // next free stage buffer
     PROF_MARK(120 + 24 * (t + 1) + 1);
-    stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
+    if (!cell_pre) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
     stage64_store(lds + b0 * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
     __syncthreads();
     f32x16 hold;
@@ -1207,7 +1243,12 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
     for (int m = 0; m < 20; ++m) {
         const f32x16 cpre = load_c(m);                           // before the staging loads (in-order vmcnt)
         __builtin_amdgcn_sched_barrier(0);
-        if (m < 19) stage64_load(csrc(m + 1), c.wave * 64 + lane_fresh(), s64);
+        if (m < 19) {
+            stage64_load(csrc(m + 1), c.wave * 64 + lane_fresh(), s64);
+        } else if (PREFETCH && t >= 0) {                         // the next step's first logit tile
+            const LaneOffs lo_ = lane_offs(c.wave, 128u);
+            stage64_load_o(logit_src(p, nidx, 0), lo_, c.wave < 2, s64);
+        }
         const float* buf = lds + ((m + b0) & 1) * STAGE64_FLOATS;
         f32x16 a0, a1;
         if (t < 0)      // h = 0 before the first cell: h2h(h) is its bias (fma(w, 0, acc) == acc)
@@ -1219,6 +1260,7 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         __syncthreads();
         PROF_MARK(120 + 24 * (t + 1) + 2 + m);
     }
+    pre = PREFETCH && t >= 0;
     PROF_MARK(2 * (t + 1) + 1);
     return true;
 }
@@ -1229,7 +1271,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
     const Ctx c = make_ctx(p);
     if (t > 0 && p.alive[c.wg] == 0) return;
     wave_prio(c.wave);
-    step_body<PAIRS>(p, c, lds, t);
+    Stage64Regs s64;
+    bool pre = false;
+    step_body<PAIRS, false>(p, c, lds, t, s64, pre);
 }
 
 // The whole decode of a workgroup (steps t = -1 .. T) in one launch: a member's steps depend only on
@@ -1243,8 +1287,10 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodePar
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const Ctx c = make_ctx(p);
     wave_prio(c.wave);
+    Stage64Regs s64;
+    bool pre = false;
     for (int t = -1; t <= p.T; ++t)
-        if (!step_body<PAIRS>(p, c, lds, t)) break;
+        if (!step_body<PAIRS, LOGIT_MIDSTORE && CROSS_PREFETCH>(p, c, lds, t, s64, pre)) break;
 }
 
 // ========== split path: one member step over several workgroups =================================
@@ -1285,7 +1331,8 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_logit_kernel(DecodePar
     for (int i = 0; i < 64; ++i) pin(hB[i]);
     RowState st;
     row_state_init(st);
-    if (s1 > s0) logit_stages<G, PAIRS>(lds, p, nidx, c.wave, c.sgn, c.hf, hB, s0, s1, st);
+    Stage64Regs s64;
+    if (s1 > s0) logit_stages<G, PAIRS>(lds, p, nidx, c.wave, c.sgn, c.hf, hB, s0, s1, st, s64);
     float* pb = part_ptr(p, c.wg, c.q, c.wave) + lane_fresh();
     pb[0] = st.m;
     pb[64] = st.s;
