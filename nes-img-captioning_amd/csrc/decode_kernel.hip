@@ -66,6 +66,9 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef CROSS_PREFETCH
 #define CROSS_PREFETCH 1   // steps kernel: a phase's first staging tile loaded during the previous phase's last stage
 #endif
+#ifndef H_PREFETCH
+#define H_PREFETCH 1       // steps kernel: h_{t+1} read back from lane scratch at the end of step t
+#endif
 #ifndef LOGIT_MIDSTORE
 #define LOGIT_MIDSTORE 1   // logit stages: the next stage's W+- tile is stored among the MFMAs of this one
 #endif
@@ -1066,20 +1069,22 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img64_kernel(DecodePar
 // logit tile, loaded during the previous step's last cell stage (PREFETCH: that load is issued)
 template <bool PAIRS, bool PREFETCH>
 __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, float* lds, int t, Stage64Regs& s64,
-                                          bool& pre) {
+                                          bool& pre, float (&hB)[64], bool& hpre) {
     PROF_MARK(2 * (t + 1));
     const uint32_t lo = 4u * c.lane;
     const int nst = (p.V1 + 63) >> 6;
     const int nl = t > 0 ? nst : 0;
     const uint64_t nidx = p.noise_idx[c.member];
-    float hB[64];
+    // the row's unfinished flag, read now: the token phase needs it right after the logit loop
+    const float unf_prev = nl > 0 ? ld1(c.scr_r, lo, U_SLOT) : 0.f;
     if (t < 0) {
 #pragma unroll
         for (int i = 0; i < 64; ++i) hB[i] = 0.f;               // h = 0 before the first cell
-    } else {
+    } else if (!hpre) {                                          // (hpre: loaded at the end of the last step)
 #pragma unroll
         for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, H_SLOT(i));
     }
+    hpre = false;
 #pragma unroll
     for (int i = 0; i < 64; ++i) pin(hB[i]);
     const uint32_t ib = (uint32_t)p.off_i2h_b, hb = (uint32_t)p.off_h2h_b, bmin = min(ib, hb);
@@ -1162,7 +1167,7 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         // end the caption instead of emitting an out-of-vocabulary id
         if (tok >= p.V1) tok = 0;
         // finished mask (nets.py:236-243)
-        const bool unfinished = ld1(c.scr_r, lo, U_SLOT) != 0.f && tok > 0;
+        const bool unfinished = unf_prev != 0.f && tok > 0;
         it = unfinished ? tok : 0;
         st1(c.scr_r, lo, U_SLOT, unfinished ? 1.f : 0.f);
 #if !DECODE_PROF
@@ -1261,6 +1266,11 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         PROF_MARK(120 + 24 * (t + 1) + 2 + m);
     }
     pre = PREFETCH && t >= 0;
+    if (PREFETCH && H_PREFETCH && t + 1 <= p.T) {                // h_{t+1}: this lane's own h' stores, read back
+#pragma unroll                                                  // while the next step's prologue runs
+        for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, H_SLOT(i));
+        hpre = true;
+    }
     PROF_MARK(2 * (t + 1) + 1);
     return true;
 }
@@ -1272,8 +1282,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
     if (t > 0 && p.alive[c.wg] == 0) return;
     wave_prio(c.wave);
     Stage64Regs s64;
-    bool pre = false;
-    step_body<PAIRS, false>(p, c, lds, t, s64, pre);
+    bool pre = false, hpre = false;
+    float hB[64];
+    step_body<PAIRS, false>(p, c, lds, t, s64, pre, hB, hpre);
 }
 
 // The whole decode of a workgroup (steps t = -1 .. T) in one launch: a member's steps depend only on
@@ -1288,9 +1299,10 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodePar
     const Ctx c = make_ctx(p);
     wave_prio(c.wave);
     Stage64Regs s64;
-    bool pre = false;
+    bool pre = false, hpre = false;
+    float hB[64];
     for (int t = -1; t <= p.T; ++t)
-        if (!step_body<PAIRS, LOGIT_MIDSTORE && CROSS_PREFETCH>(p, c, lds, t, s64, pre)) break;
+        if (!step_body<PAIRS, LOGIT_MIDSTORE && CROSS_PREFETCH>(p, c, lds, t, s64, pre, hB, hpre)) break;
 }
 
 // ========== split path: one member step over several workgroups =================================
