@@ -761,9 +761,11 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
         const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * sgn;
         auto mid = [&]() __attribute__((always_inline)) {
 #if LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
+            // s64 is loaded on every non-last path (at s1 - 2 the load repeats tile s1 - 1): a conditional load
+            // here would make the compiler copy the 32 staging registers at every stage to merge the paths
             if (s + 1 < s1) {
                 stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
-                if (s + 2 < s1) stage64_load_o(lsrc(s + 2), lo, bias, s64);
+                stage64_load_o(lsrc(min(s + 2, s1 - 1)), lo, bias, s64);
             } else {
                 tail();
             }
