@@ -4,14 +4,18 @@
 One step = one full NES iteration over the population on synthetic inputs resident in HBM:
 perturb (in LDS) + greedy decode of both antithetic candidates of every member + CIDEr-D fitness,
 fitness all-gather, centred ranks, weighted noise sum, gradient all-reduce, Adam.
-Workload (BASELINE.json configs[2], 'mscoco_nes.json fc_caption, pop=512 antithetic,
-batch_size=128'): 512 members per GPU, 128 unique images, sigma 0.01, l2coeff 1e-7, Adam 1e-3.
-Multi-GPU is weak scaling: each rank evaluates its own 512 members of a population of 512*N
-(configs[3]'s pop=2048 on 8 GPUs has 256 per GPU; --pop-per-gpu 256 runs that).
+Workload (BASELINE.json metric, 'fc_caption, pop=512 ... at 1/2/4/8 GPUs'; configs[2] at N = 1):
+a population of 512 members, 128 unique images, sigma 0.01, l2coeff 1e-7, Adam 1e-3.
+Multi-GPU is STRONG scaling by default, as the reference scales: more workers split a fixed
+nb_offspring (main.py:105,144-153; tools/iteration.py:173; the master waits for nb_offspring results,
+nic_nes_master.py:92-118), so rank r evaluates members [r P/N, (r+1) P/N) of the same P = 512.
+--preset names the other BASELINE configs: configs1 (pop=64), configs3 (pop=2048; 256 per GPU on 8),
+configs4 ('bu' features, pop=512; 64 per GPU on 8). --pop-per-gpu M is weak scaling (P = M N).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--preset metric|configs1|configs2|configs3|configs4]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 """
+import hashlib
 import argparse
 import json
 import os
@@ -72,19 +76,54 @@ def iteration_algorithmic_bytes(B, P, D=2865808):
     return P * (step_noise_bytes_per_member(B) + 4 * D) + 4 * D + (3 * 2 * 8 + 4 + 4) * D
 
 
-PMC_FILES = {('nicnes_decode_steps_kernel', 512, 128): 'profiles/r02_pmc_steps_p512_b128.json',
-             ('nicnes_decode_step_kernel', 512, 128): 'profiles/r02_pmc_step_p512_b128.json',
-             ('nicnes_decode_logit_kernel<4>', 64, 128): 'profiles/r02_pmc_logit_p64_b128.json'}
+# BASELINE.json configs by name: (population, batch, bu features, the config's text)
+PRESETS = {
+    'metric': (512, 128, False, 'the metric: fc_caption pop=512 at 1/2/4/8 GPUs (configs[2] at N = 1)'),
+    'configs1': (64, 128, False, 'configs[1]: mscoco_nes.json fc_caption, synthetic 2048-d fc feats, pop=64'),
+    'configs2': (512, 128, False, 'configs[2]: mscoco_nes.json fc_caption, pop=512 antithetic, batch_size=128'),
+    'configs3': (2048, 128, False, 'configs[3]: mscoco_nes.json fc_caption, pop=2048 sharded (256 per GPU on 8)'),
+    'configs4': (512, 128, True, "configs[4]: mscoco_nes.json with 'bu' features, pop=512 (64 per GPU on 8)"),
+}
+
+# committed PMC profiles: profiles/<round>_pmc_<key>_p<members per GPU>_b<B>.json
+PMC_KEYS = {'nicnes_decode_steps_kernel': 'steps', 'nicnes_decode_step_kernel': 'step',
+            'nicnes_decode_logit_kernel<4>': 'logit', 'nicnes_decode_coop_kernel<4>': 'coop4',
+            'nicnes_decode_coop_kernel<2>': 'coop2', 'nicnes_decode_steps2_kernel': 'steps2'}
+KERNEL_SOURCES = ('nes-img-captioning_amd/csrc/decode_kernel.hip', 'nes-img-captioning_amd/csrc/decode_kernel.h',
+                  'include/nicnes_math.h')
+
+
+def kernel_source_sha256():
+    """Hash of the decode kernel's sources: a PMC profile records it, and bench.py uses the profile's
+    counter figures only while the sources still hash the same."""
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(REPO, f), 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 
 
 def load_pmc(kernel, P, B):
-    f = PMC_FILES.get((kernel, P, B))
-    if not f or not os.path.exists(os.path.join(REPO, f)):
-        return None
-    with open(os.path.join(REPO, f)) as fh:
-        rec = json.load(fh)
-    rec['file'] = f
-    return rec
+    """The newest committed PMC profile of (kernel, members per GPU, B) whose recorded source hash is
+    the current one; (None, reason) when there is none (stale counters are never reported)."""
+    import glob
+    key = PMC_KEYS.get(kernel)
+    if key is None:
+        return None, None
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_%s_p%d_b%d.json' % (key, P, B))), reverse=True)
+    if not files:
+        return None, None
+    sha = kernel_source_sha256()
+    for f in files:
+        with open(f) as fh:
+            rec = json.load(fh)
+        if rec.get('source_sha256') == sha:
+            rec['file'] = os.path.relpath(f, REPO)
+            return rec, None
+    reason = ('%s records kernel source %s, the tree has %s: counters not reported (re-run the PMC passes)'
+              % (os.path.relpath(files[0], REPO), str(rec.get('source_sha256'))[:12], sha[:12]))
+    print('bench.py: STALE PMC PROFILE: ' + reason, file=sys.stderr, flush=True)
+    return None, reason
 
 
 def cpu_baseline(args, B, P):
@@ -135,8 +174,11 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--pop-per-gpu', type=int, default=512)
-    ap.add_argument('--batch', type=int, default=128)
+    ap.add_argument('--preset', choices=sorted(PRESETS), default='metric', help='BASELINE.json config')
+    ap.add_argument('--population', type=int, default=0, help='total population P, split over the N GPUs '
+                    '(strong scaling; default: the preset\'s, 512 for the metric)')
+    ap.add_argument('--pop-per-gpu', type=int, default=0, help='weak scaling instead: members per GPU (P = N x this)')
+    ap.add_argument('--batch', type=int, default=0, help='unique images per batch (default: the preset\'s, 128)')
     ap.add_argument('--theta-gain', type=float, default=1.0, help='weight init gain (1: the reference xavier init; '
                     '4 with --bias-std 0.1: peaked, trained-like logits)')
     ap.add_argument('--bias-std', type=float, default=0.0)
@@ -144,7 +186,8 @@ def main():
                     'member i on batch i mod N)')
     ap.add_argument('--sigma', type=float, default=0.01)
     ap.add_argument('--noise-len', type=int, default=1 << 27)
-    ap.add_argument('--bu', action='store_true', help="'bu' features: ReLU(N(0,1)) fc (configs[4])")
+    ap.add_argument('--bu', action='store_true', help="'bu' features: ReLU(N(0,1)) fc (configs[4]; implied by "
+                    "--preset configs4)")
     ap.add_argument('--fitness', default='greedy', help="policy_options.fitness: greedy (mscoco_nes.json) or "
                     "greedy_logprob / greedy_expprob / greedy_linprob / greedy_avgprob")
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -157,12 +200,22 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    B = args.batch
+    P_pre, B_pre, bu_pre, cfg_text = PRESETS[args.preset]
+    B = args.batch or B_pre
+    args.bu = args.bu or bu_pre
+    if args.pop_per_gpu:                     # weak scaling: a fixed share per GPU
+        P_local, scaling = args.pop_per_gpu, 'weak'
+        P = P_local * world
+    else:                                    # strong scaling: a fixed population split over the GPUs
+        P, scaling = args.population or P_pre, 'strong'
+        if P % world:
+            raise SystemExit('population %d does not split evenly over %d GPUs' % (P, world))
+        P_local = P // world
 
     # CPU leg first, before this process touches the GPU (its pool forks)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, B, args.pop_per_gpu)
+        cpu = cpu_baseline(args, B, P)
 
     import torch
     import torch.distributed as dist
@@ -180,8 +233,6 @@ def main():
             dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
         else:
             dist.init_process_group(backend)
-    P_local = args.pop_per_gpu
-    P = P_local * world
     eng = nicnes.Engine(max_batch=B, max_members=P_local, noise_len=args.noise_len, noise_seed=0,
                         device=dev)
     S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu, batches=args.batches,
@@ -247,18 +298,21 @@ def main():
     achieved = step_flop / (step_ms / 1e3) / 1e12
     # counter figures of the same kernel and workload from the committed rocprofv3 PMC profile
     # (a profile-derived constant: PMC passes cannot run inside the timed bench process)
-    pmc = load_pmc(kname, P_local, B)
+    pmc, pmc_stale = load_pmc(kname, P_local, B)
     traffic = pmc['derived'].get('hbm_bytes_per_launch') if pmc else None
     hbm_peak_bytes = HBM_PEAK_GBS * 1e9 * step_ms / 1e3
     iter_bytes = iteration_algorithmic_bytes(B, P_local)
     out = {
         'metric': METRIC, 'value': round(value, 3), 'unit': 'members/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(dt / args.steps * 1e3, 3), 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+        'scaling': scaling, 'vs_baseline': None, 'dtype': 'fp32',
         'data': 'synthetic (seeded fc features, xavier-init fc_caption theta, substituted refs, 2^27 noise table)',
-        'config': {'workload': 'mscoco_nes.json fc_caption, pop=%d antithetic (%d/GPU), batch_size=%d unique '
+        'config': {'baseline_config': args.preset if not (args.population or args.pop_per_gpu or args.batch)
+                   else 'custom (%s preset overridden)' % args.preset,
+                   'baseline_config_text': cfg_text,
+                   'workload': 'mscoco_nes.json fc_caption, pop=%d antithetic (%d/GPU, %s scaling), batch_size=%d unique '
                                'images, sigma %.3g, full iteration (decode+CIDEr-D+ranks+noise sum+Adam)'
-                               % (P, P_local, B, args.sigma) + (", 'bu' fc features" if args.bu else '')
+                               % (P, P_local, scaling, B, args.sigma) + (", 'bu' fc features" if args.bu else '')
                                + (', fitness %s' % args.fitness if args.fitness != 'greedy' else '')
                                + (', theta gain %g bias std %g (not the reference init)' % (args.theta_gain, args.bias_std)
                                   if (args.theta_gain != 1.0 or args.bias_std) else '')
@@ -278,6 +332,7 @@ def main():
                      'algorithmic_bytes_per_launch': alg_bytes,
                      'traffic_over_algorithmic': (round(traffic / alg_bytes, 3) if traffic else None),
                      'traffic_source': pmc['file'] if pmc else None,
+                     'traffic_stale': pmc_stale,
                      'hbm_frac': round(alg_bytes / hbm_peak_bytes, 4),
                      'hbm_frac_counters': round(traffic / hbm_peak_bytes, 4) if traffic else None,
                      'mfma_busy': round(pmc['derived']['mfma_busy'], 4) if pmc and 'mfma_busy' in pmc['derived'] else None,

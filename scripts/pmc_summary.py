@@ -19,6 +19,10 @@ import csv
 import glob
 import json
 import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402  (kernel_source_sha256: the profile records which decode sources it measured)
 
 
 def per_dispatch(root, kernel):
@@ -64,7 +68,8 @@ def main():
             counters[name] = v
             dispatches[name] = n
     c = counters
-    out = {'kernel': a.kernel, 'note': a.note, 'counters_per_launch': c, 'dispatches': dispatches}
+    out = {'kernel': a.kernel, 'note': a.note, 'source_sha256': bench.kernel_source_sha256(),
+           'counters_per_launch': c, 'dispatches': dispatches}
     d = {}
     if 'FETCH_SIZE' in c and 'WRITE_SIZE' in c:
         d['hbm_bytes_per_launch'] = (2.0 * c['FETCH_SIZE'] + c['WRITE_SIZE']) * 1024.0
