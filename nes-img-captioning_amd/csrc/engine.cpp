@@ -20,6 +20,8 @@
 #include "decode_kernel.h"
 #include "update_kernels.h"
 
+#define MB_RING 4   // pinned staging slots of the member -> batch map (nicnes_evaluate_batches)
+
 struct nicnes_handle {
     nicnes_config cfg;
     int device = 0;
@@ -45,6 +47,12 @@ struct nicnes_handle {
     int32_t n_img = 0;                // images held = n_batches * B
     int32_t img_cap = 0;              // per-image CIDEr-D table capacity
     int32_t* mbatch = nullptr;        // [max_members] member -> batch map of the current evaluate
+    // the caller's host map is staged in a ring of pinned buffers (each reused only after its copy has
+    // run, told by its event), so an evaluate with a map never waits for the queued GPU work
+    int32_t* mb_pin[MB_RING] = {};
+    hipEvent_t mb_ev[MB_RING] = {};
+    bool mb_used[MB_RING] = {};
+    int mb_next = 0;
     int32_t n_refs = 0;
     const int32_t* img_ref_start = nullptr;
     bool batch_set = false;
@@ -345,6 +353,12 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
     if (!rc) rc = alloc_batch(h, cfg->max_batch);
     if (!rc) rc = alloc_images(h, cfg->max_batch);
     if (!rc) rc = dalloc(h, &h->mbatch, (size_t)cfg->max_members);
+    for (int i = 0; i < MB_RING && !rc; ++i) {
+        if (hipHostMalloc((void**)&h->mb_pin[i], (size_t)cfg->max_members * sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
+            rc = fail(h, NICNES_ERR_HIP, "hipHostMalloc");
+        else if (hipEventCreateWithFlags(&h->mb_ev[i], hipEventDisableTiming) != hipSuccess)
+            rc = fail(h, NICNES_ERR_HIP, "hipEventCreate");
+    }
     if (rc) {
         nicnes_destroy(h);
         return rc;
@@ -373,6 +387,13 @@ int nicnes_destroy(nicnes_handle* h) {
     if (h->stats_pending) (void)hipEventSynchronize(h->stats_ev);
     if (h->stats_host) (void)hipHostFree(h->stats_host);
     if (h->stats_ev) (void)hipEventDestroy(h->stats_ev);
+    for (int i = 0; i < MB_RING; ++i) {
+        if (h->mb_ev[i]) {
+            (void)hipEventSynchronize(h->mb_ev[i]);
+            (void)hipEventDestroy(h->mb_ev[i]);
+        }
+        if (h->mb_pin[i]) (void)hipHostFree(h->mb_pin[i]);
+    }
     for (hipEvent_t e : h->ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : h->dev)
@@ -627,8 +648,14 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
         for (int k = 0; k < count; ++k)
             if (member_batch_host[k] < 0 || member_batch_host[k] >= h->n_batches)
                 return fail(h, NICNES_ERR_INVALID, "member_batch entry outside [0, n_batches)");
-        HIPC(h, hipMemcpyAsync(h->mbatch, member_batch_host, (size_t)count * sizeof(int32_t), hipMemcpyHostToDevice, s));
-        HIPC(h, hipStreamSynchronize(s));        // the caller's host array may go away on return
+        // the caller's array may go away on return: copied to a pinned ring slot whose previous copy has run
+        const int slot = h->mb_next;
+        h->mb_next = (slot + 1) % MB_RING;
+        if (h->mb_used[slot]) HIPC(h, hipEventSynchronize(h->mb_ev[slot]));
+        std::memcpy(h->mb_pin[slot], member_batch_host, (size_t)count * sizeof(int32_t));
+        HIPC(h, hipMemcpyAsync(h->mbatch, h->mb_pin[slot], (size_t)count * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        HIPC(h, hipEventRecord(h->mb_ev[slot], s));
+        h->mb_used[slot] = true;
         mb = h->mbatch;
     } else if (h->n_batches != 1) {
         return fail(h, NICNES_ERR_INVALID, "several batches are held: pass member_batch (nicnes_evaluate_batches)");

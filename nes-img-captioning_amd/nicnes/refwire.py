@@ -10,8 +10,9 @@ result.fitness / result.evolve_noise / result.eval_score (nic_nes_master.py:92-1
                (algorithm.nic_nes.nic_nes_master.NESTask / NESResult), written without importing
                the reference: RefNESTask / RefNESResult carry the reference's module path, and the
                pickler emits that path for them. Everything else (numpy arrays, dicts, floats) is
-               pickled as the reference pickles it, byte for byte (tests/test_refwire.py checks the
-               bytes against the reference's own dist.serialize output, tests/golden/wire_reference.npz).
+               pickled as the reference pickles it, byte for byte (tests/test_worker_entry.py,
+               test_engine_results_are_the_reference_bytes, checks the bytes against the reference's own
+               dist.serialize output, tests/golden/wire_reference.npz).
   loads(b)     a restricted unpickler: the reference wire types map to RefNESTask / RefNESResult, and
                only numpy array / scalar reconstruction and a few plain containers are admitted; any
                other global (os.system, builtins.eval, ...) is refused, so decoding never runs code.
@@ -19,10 +20,16 @@ result.fitness / result.evolve_noise / result.eval_score (nic_nes_master.py:92-1
   run_reference_worker
                NESWorker.run_worker (nic_nes_worker.py:41-90) on the engine: members in chunks, each
                result in the reference format with its evolve_noise = fp32(sigma * z) materialised
-               from the shared table (nicnes_noise_vectors), and with probability eval_prob an eval
-               result (the greedy CIDEr-D fitness of the unperturbed theta on the task batch stands in
-               for the COCO validation eval, which needs java and the val set: out of scope).
+               from the shared table (nicnes_noise_vectors). Each claimed slot of a chunk is, with
+               probability eval_prob, an eval result instead of a member, as each reference worker
+               iteration is (nic_nes_worker.py:65): the greedy CIDEr-D fitness of the unperturbed theta
+               on the task batch stands in for the COCO validation eval, which needs java and the val
+               set (out of scope).
+               Difference from reference workers with single_batch: false (mscoco_nes.json's setting):
+               they score each member on a batch of their own loader (nic_nes_worker.py:121-128); this
+               worker scores every member on the master's published batch (a warning is logged).
 """
+import logging
 import io
 import os
 import pickle
@@ -148,15 +155,36 @@ def reference_results(worker, task_id, task, member_begin, count):
                          fitness=np.asarray(r.fitness, np.float64), mem_usage=mem) for k, r in enumerate(res)]
 
 
+# what the reference worker survives (nic_nes_worker.py:71-84: the master deletes and rewrites the current
+# parameter file between iterations, so a late reader can find it missing or half written)
+TRANSIENT_ERRORS = (FileNotFoundError, EOFError, RuntimeError)
+
+
+def chunk_evals(rs, chunk, eval_prob):
+    """How many of a chunk's `chunk` slots are eval runs: one eval_prob coin per slot, as one per
+    reference worker iteration (nic_nes_worker.py:65), so the master sees eval results at the
+    reference's rate per result whatever the chunk size."""
+    if not eval_prob:
+        return 0
+    return sum(1 for _ in range(chunk) if rs.random() < eval_prob)
+
+
 def run_reference_worker(client, worker, chunk=16, eval_prob=0.0, max_tasks=None, stop=None, seed=None,
-                         idle_sleep=0.005, max_results=None):
+                         idle_sleep=0.005, max_results=None, retry_sleep=0.05):
     """NESWorker.run_worker (nic_nes_worker.py:41-90) against a reference master: `client` is a
-    nicnes.transport.WorkerClient built with codec=RefPickleCodec. Members of a task are claimed in
-    chunks from a per-task counter in the same store (the reference's workers draw their noise
-    independently; the engine needs distinct noise indices); results of a task keep flowing until
-    the master declares the next one, as reference workers do (surplus results are dropped by the
-    master, nic_nes_master.py:108-116). Returns the number of tasks seen."""
+    nicnes.transport.WorkerClient built with codec=RefPickleCodec. Each pass takes `chunk` slots:
+    chunk_evals of them are eval results (one rollout of the unperturbed theta, pushed once per eval
+    slot), the rest are members claimed from a per-task counter in the same store (the reference's
+    workers draw their noise independently; the engine needs distinct noise indices). Results of a
+    task keep flowing until the master declares the next one, as reference workers do (surplus results
+    are dropped by the master, nic_nes_master.py:108-116). A missing or half-written parameter file is
+    logged and the task re-read, as nic_nes_worker.py:71-84 does. Returns the number of tasks seen."""
     rs = random.Random(seed)
+    log = logging.getLogger(__name__)
+    spec = getattr(worker, 'spec', None)
+    if spec is not None and not getattr(spec, 'single_batch', True):
+        log.warning('single_batch is false: reference workers score each member on a batch of their own loader '
+                    '(nic_nes_worker.py:121-128); this worker scores every member on the published batch')
     seen, pushed = set(), 0
     while not (stop is not None and stop.is_set()):
         task_id, ref_task = client.get_current_task()
@@ -164,14 +192,22 @@ def run_reference_worker(client, worker, chunk=16, eval_prob=0.0, max_tasks=None
             return len(seen)
         seen.add(task_id)
         task = to_engine_task(ref_task, task_id)
-        if eval_prob and rs.random() < eval_prob:
-            worker._prepare(task_id, task)
-            score = worker.policy.rollout(None, task.batch_data, None)
-            client.push_result(task_id, RefNESResult(worker_id=worker.worker_id, eval_score=score, mem_usage=_rss()))
+        n_eval = chunk_evals(rs, chunk, eval_prob)
+        try:
+            if n_eval:
+                worker._prepare(task_id, task)
+                score = worker.policy.rollout(None, task.batch_data, None)
+                ev = RefNESResult(worker_id=worker.worker_id, eval_score=score, mem_usage=_rss())
+                client.push_results(task_id, [ev] * n_eval)
+                pushed += n_eval
+            if chunk > n_eval:
+                begin = client.claim_members(task_id, chunk - n_eval)
+                client.push_results(task_id, reference_results(worker, task_id, task, begin, chunk - n_eval))
+                pushed += chunk - n_eval
+        except TRANSIENT_ERRORS as e:
+            log.error('task %s: %s (re-reading the task)', task_id, e)
+            time.sleep(retry_sleep)
             continue
-        begin = client.claim_members(task_id, chunk)
-        client.push_results(task_id, reference_results(worker, task_id, task, begin, chunk))
-        pushed += chunk
         if max_results is not None and pushed >= max_results:
             return len(seen)
         time.sleep(idle_sleep)

@@ -253,10 +253,11 @@ class TCPStoreRedis:
         return self.s.get(k) if self.s.check([k]) else None
 
     def mset(self, mapping):
+        # the snapshot first: a reader that sees a new individual key finds a snapshot holding it
         vals = {k: (v if isinstance(v, bytes) else str(v).encode()) for k, v in mapping.items()}
+        self.s.set(self._SNAP, msgpack.packb(vals, use_bin_type=True))
         for k, v in vals.items():
             self.s.set(k, v)
-        self.s.set(self._SNAP, msgpack.packb(vals, use_bin_type=True))
         return True
 
     def mget(self, keys):
@@ -388,13 +389,21 @@ class WorkerClient:
     def get_experiment(self):
         return self.codec.deserialize(_retry_get(self.local_redis, EXP_KEY))
 
-    def get_current_task(self):
-        task_id = int(_retry_get(self.local_redis, TASK_ID_KEY))
-        if task_id != self.cached_task_id:
+    def get_current_task(self, retry_sleep=0.01):
+        """(task_id, task). A task caught half published (its id without its data, or the pair read
+        across two declarations) is not taken: the previous task is served meanwhile, or, before the
+        first task, the read is retried."""
+        while True:
+            task_id = int(_retry_get(self.local_redis, TASK_ID_KEY))
+            if task_id == self.cached_task_id:
+                return self.cached_task_id, self.cached_task_data
             tid, data = self.local_redis.mget([TASK_ID_KEY, TASK_DATA_KEY])
-            if int(tid) == task_id:
+            if tid is not None and data is not None and int(tid) == task_id:
                 self.cached_task_id, self.cached_task_data = task_id, self.codec.deserialize(data)
-        return self.cached_task_id, self.cached_task_data
+                return self.cached_task_id, self.cached_task_data
+            if self.cached_task_id is not None:
+                return self.cached_task_id, self.cached_task_data
+            time.sleep(retry_sleep)
 
     def claim_members(self, task_id, count):
         """Atomically reserve member ids [begin, begin+count) of this task (new; members = noise indices)."""

@@ -50,7 +50,8 @@ def parse_args(argv=None):
     ap.add_argument('--eval_prob', type=float, default=None, help='reference wire: default config.eval_prob')
     ap.add_argument('--engine_factory', default='nicnes.worker:default_engine')
     ap.add_argument('--check_interval', type=float, default=60.0)
-    ap.add_argument('--max_restarts', type=int, default=20)
+    ap.add_argument('--max_restarts', type=int, default=20, help='restarts allowed within --restart_window seconds')
+    ap.add_argument('--restart_window', type=float, default=3600.0)
     ap.add_argument('--max_tasks', type=int, default=None)
     return ap.parse_args(argv)
 
@@ -130,6 +131,22 @@ def _visible_gpus():
         return 0
 
 
+class RestartBudget:
+    """At most `max_restarts` restarts within any `window` seconds (a rate, not a lifetime total: a
+    long run that loses a worker now and then, e.g. to the parameter-file race of
+    nic_nes_worker.py:71-84, keeps its pool)."""
+
+    def __init__(self, max_restarts, window):
+        self.max, self.window, self.times = int(max_restarts), float(window), []
+
+    def allow(self, now):
+        self.times = [t for t in self.times if now - t < self.window]
+        if len(self.times) >= self.max:
+            return False
+        self.times.append(now)
+        return True
+
+
 def supervise(args):
     """Start one worker per GPU, restart dead ones as fresh processes, stop on SIGINT / SIGTERM or
     the store's stop key. Returns the number of restarts."""
@@ -154,13 +171,14 @@ def supervise(args):
     for sig in (signal.SIGINT, signal.SIGTERM):
         signal.signal(sig, lambda *_: stopping.set())
     restarts = 0
+    budget = RestartBudget(args.max_restarts, getattr(args, 'restart_window', 3600.0))
     try:
         while not stopping.is_set():
             if store.get(STOP_KEY) is not None:
                 break
             for i, p in list(procs.items()):
                 if not p.is_alive():
-                    if restarts >= args.max_restarts:
+                    if not budget.allow(time.monotonic()):
                         logging.warning('worker %d died (exit %s); restart budget spent', i, p.exitcode)
                         stopping.set()
                         break

@@ -165,3 +165,117 @@ def test_worker_pool_restarts_and_serves_the_engine_master(tmp_path):
     finally:
         if pool.poll() is None:
             os.killpg(pool.pid, signal.SIGKILL)
+
+
+def test_eval_results_arrive_at_eval_prob_per_member(tmp_path):
+    """Each slot of a chunk is an eval run with probability eval_prob (one coin per reference worker
+    iteration, nic_nes_worker.py:65), so a reference master, which finishes an iteration only once it
+    has nb_offspring evolve results AND an eval result of the current task (nic_nes_master.py:92-118,
+    nic_nes/iteration.py:49-50), sees them at the reference's rate whatever the chunk size."""
+    dims, theta, fc, gts, df, n, table = tiny_workload()
+    path = str(tmp_path / '0_current_params.pth')
+    eng = OracleEngine(dims, theta, fc, gts, df, n, table)
+    torch.save(N.state_dict_from_vector(torch.from_numpy(theta), N.param_shapes(eng)), path)
+    store = T.LocalStore()
+    mc = T.MasterClient(store, codec=W.RefPickleCodec)
+    mc.declare_experiment(_spec(4).exp)
+    batch = {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts}
+    tid = mc.declare_task(W.RefNESTask(current=path, batch_data=batch, noise_stdev=0.05, log_dir=str(tmp_path),
+                                       batch_size=4))
+    worker = N.EngineWorker(eng, _spec(4), worker_id=5)
+    # stand-ins that keep 2,000+ slots fast: the counting is what is under test here
+    worker.fitness_batch = lambda t, task, b, c: [N.NESResult(worker_id=5, fitness=np.zeros(2), noise_idx=0, member=b + k)
+                                                  for k in range(c)]
+    worker.e.noise_vectors = lambda it, b, c, s: torch.zeros((c, 4))
+    nb_offspring, p = 2000, 0.05
+    stop = threading.Event()
+    th = threading.Thread(target=W.run_reference_worker, daemon=True,
+                          args=(T.WorkerClient(store, codec=W.RefPickleCodec), worker),
+                          kwargs=dict(chunk=64, eval_prob=p, seed=1, stop=stop, idle_sleep=0.0))
+    th.start()
+    evolve, evals = 0, 0
+    try:
+        # the reference master's loop for one iteration
+        while evolve < nb_offspring or evals == 0:
+            t, r = mc.pop_result(timeout=60)
+            assert t == tid, 'no result within 60 s'
+            if r.eval_score is not None:
+                evals += 1
+            else:
+                evolve += 1
+    finally:
+        stop.set()
+        th.join(60)
+    total = evolve + evals
+    sd = (total * p * (1 - p)) ** 0.5
+    assert abs(evals - p * total) < 5 * sd, (evals, total)
+    assert nb_offspring <= evolve < nb_offspring + 64        # the iteration ends within one chunk
+
+
+def test_reference_worker_survives_a_missing_parameter_file(tmp_path):
+    """The master deletes and rewrites current/0_current_params.pth between iterations
+    (nic_nes/iteration.py:54-55); a late worker logs the error and re-reads the task
+    (nic_nes_worker.py:71-84) instead of dying."""
+    dims, theta, fc, gts, df, n, table = tiny_workload()
+    eng = OracleEngine(dims, theta, fc, gts, df, n, table)
+    path = str(tmp_path / '0_current_params.pth')
+    store = T.LocalStore()
+    mc = T.MasterClient(store, codec=W.RefPickleCodec)
+    mc.declare_experiment(_spec(4).exp)
+    batch = {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts}
+    tid = mc.declare_task(W.RefNESTask(current=path, batch_data=batch, noise_stdev=0.05, log_dir=str(tmp_path),
+                                       batch_size=4))
+    worker = N.EngineWorker(eng, _spec(4), worker_id=6)
+    stop = threading.Event()
+    th = threading.Thread(target=W.run_reference_worker, daemon=True,
+                          args=(T.WorkerClient(store, codec=W.RefPickleCodec), worker),
+                          kwargs=dict(chunk=2, seed=0, stop=stop, retry_sleep=0.01))
+    th.start()
+    try:
+        time.sleep(0.3)                                       # the file is missing meanwhile
+        assert th.is_alive() and mc.pop_result(timeout=0.01)[0] is None
+        torch.save(N.state_dict_from_vector(torch.from_numpy(theta), N.param_shapes(eng)), path + '.tmp')
+        os.replace(path + '.tmp', path)
+        t, r = mc.pop_result(timeout=60)
+        assert t == tid and r.fitness is not None
+    finally:
+        stop.set()
+        th.join(60)
+
+
+def test_restart_budget_is_a_rate():
+    from nicnes.worker import RestartBudget
+    b = RestartBudget(2, 10.0)
+    assert b.allow(0.0) and b.allow(1.0) and not b.allow(2.0)
+    assert b.allow(11.5)                                      # the first restart left the window
+
+
+def test_half_published_task_is_not_taken():
+    """TCPStoreRedis writes its snapshot before the individual keys, and a worker that still catches
+    an id without its data keeps serving its previous task (or retries before the first one)."""
+    class Half:
+        def __init__(self):
+            self.kv = {}
+
+        def get(self, k):
+            return self.kv.get(k)
+
+        def mget(self, keys):
+            return [self.kv.get(k) for k in keys]
+
+        def rpush(self, k, *v):
+            return 0
+
+    s = Half()
+    wc = T.WorkerClient(s)
+    codec = wc.codec
+    s.kv[T.TASK_ID_KEY] = b'1'
+    s.kv[T.TASK_DATA_KEY] = codec.serialize(N.NESTask(noise_stdev=0.5))
+    assert wc.get_current_task()[0] == 1
+    s.kv[T.TASK_ID_KEY] = b'2'                                # id published, data still the old task's
+    s.kv.pop(T.TASK_DATA_KEY)
+    tid, task = wc.get_current_task()
+    assert tid == 1 and task.noise_stdev == 0.5
+    s.kv[T.TASK_DATA_KEY] = codec.serialize(N.NESTask(noise_stdev=0.25))
+    tid, task = wc.get_current_task()
+    assert tid == 2 and task.noise_stdev == 0.25
