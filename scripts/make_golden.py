@@ -21,9 +21,12 @@ Fixtures (all .npz, loadable with allow_pickle=False):
   decode_bench_xavier.npz         the bench workload itself (BASELINE.json configs[2] inputs: xavier theta seed
                                   0, fc PCG64(1234) [128, 2048], the 2^27 table PCG64(123), noise seed 0,
                                   iteration 1): FCModel._sample on the reference's 5x-duplicated 640 rows
-                                  (dataloader.py:175) for base theta and 8 table-perturbed members x 2 signs;
+                                  (dataloader.py:175) for base theta and 16 table-perturbed members x 2 signs
+                                  (8 of them below 64, so the pop=64 split path is pinned on 2,048 rows);
                                   tokens of each image's first copy, per-step top-2 margins, logprobs, and
                                   whether the 5 copies of every image decoded identically
+  decode_bench_b64.npz            the same at mscoco_nes.json's own batch_size 64 (experiments/mscoco_nes.json:7):
+                                  the first 64 images (320 duplicated rows), the 64-row slab path of the engine
   master_ranks_grad.npz           NESMaster.compute_centered_ranks / gradient_estimate
                                   (nic_nes_master.py:170-221) imported with placeholder redis/torchvision
                                   modules: P = 512 tie-free fitness and a tied one, and the fp32 gradient
@@ -138,15 +141,20 @@ def decode_fixture(name, d, theta_seed, gain, bias_std, fc_seed, B, store_theta,
     print(name, 'seq[0]', seq[0], 'min margin', float(mar.min()))
 
 
-def decode_bench_fixture():
+BENCH_MEMBERS = np.array(sorted(set(np.linspace(0, 511, 8).astype(np.int64).tolist())
+                                | {8, 16, 24, 32, 40, 48, 63, 100}), np.int64)
+
+
+def decode_bench_fixture(B=128, name='decode_bench_xavier'):
     d = O.Dims()
     model = ref_model(d)
     theta = O.make_theta(d, 0, 1.0, 0.0)               # = nicnes.synthetic.init_theta(Dims(), 0)
-    B, T_LEN, TSEED, NSEED, IT, SIGMA = 128, 1 << 27, 123, 0, 1, 0.01
+    T_LEN, TSEED, NSEED, IT, SIGMA = 1 << 27, 123, 0, 1, 0.01
+    # the first B rows of the bench's PCG64(1234) [128, 2048] draw (numpy fills in C order)
     fc = np.random.Generator(np.random.PCG64(1234)).standard_normal((B, d.F)).astype(np.float32)
     fc5 = np.repeat(fc, 5, axis=0)                     # the reference decodes every image 5 times
     table = O.noise_table(T_LEN, TSEED)
-    members = np.linspace(0, 511, 8).astype(np.int64)
+    members = BENCH_MEMBERS
     seqs, mars, lps, dup = [], [], [], []
 
     def run(th):
@@ -163,11 +171,15 @@ def decode_bench_fixture():
         idx = O.noise_index(NSEED, IT, int(mbr), T_LEN, d.D)
         for sign in (+1, -1):
             run(O.perturb(theta, table, idx, SIGMA, sign))
-    np.savez_compressed(os.path.join(OUT, 'decode_bench_xavier.npz'), B=np.int64(B), noise_len=np.int64(T_LEN),
+    np.savez_compressed(os.path.join(OUT, name + '.npz'), B=np.int64(B), noise_len=np.int64(T_LEN),
                         table_seed=np.int64(TSEED), noise_seed=np.int64(NSEED), iteration=np.int64(IT),
                         sigma=np.float64(SIGMA), members=members, seq=np.stack(seqs).astype(np.int16),
                         margins=np.stack(mars), logprobs=np.stack(lps), dup_consistent=np.array(dup))
-    print('decode_bench: copies consistent', all(dup), 'min margin', float(np.stack(mars).min()))
+    print(name, 'copies consistent', all(dup), 'min margin', float(np.stack(mars).min()))
+
+
+def decode_bench_b64_fixture():
+    decode_bench_fixture(64, 'decode_bench_b64')
 
 
 class _Placeholder(__import__('types').ModuleType):
@@ -399,6 +411,7 @@ def all_fixtures():
     adam_globalg64_fixture()
     fitness_criteria_fixture()
     decode_bench_fixture()
+    decode_bench_b64_fixture()
     master_ranks_grad_fixture()
     wire_fixture()
     mutations_fixture()
