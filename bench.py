@@ -275,6 +275,7 @@ def main():
     # averages over the same launches)
     ph = phases[-1]
     G, nslabs, S_split = eng.decode_shape(B, P_local)
+    path = eng.decode_path(B, P_local)
     if not ph['step_launches'] and not ph['logit_launches']:
         # two-stream decode (NICNES_DECODE_STREAMS=2): the halves' launches overlap, so the whole decode
         # is the measured unit
@@ -284,8 +285,12 @@ def main():
         alg_bytes = step_noise_bytes_per_member(B) * P_local
     elif ph['step_launches']:
         # fused path: every step of a workgroup in one launch (nicnes_decode_steps_kernel), or one launch
-        # per step t = -1..T (nicnes_decode_step_kernel, DECODE_PERSISTENT=0 builds)
-        kname = 'nicnes_decode_steps_kernel' if ph['step_launches'] == 1 else 'nicnes_decode_step_kernel'
+        # per step t = -1..T (nicnes_decode_step_kernel, DECODE_PERSISTENT=0 builds); coop path: the split
+        # shape's every step in one launch (nicnes_decode_coop_kernel, S workgroups per member slab)
+        if path == 'coop':
+            kname = 'nicnes_decode_coop_kernel<%d>' % S_split
+        else:
+            kname = 'nicnes_decode_steps_kernel' if ph['step_launches'] == 1 else 'nicnes_decode_step_kernel'
         n_step = ph['step_launches']
         step_ms = float(np.mean([q['step_ms'] for q in phases])) / n_step
         step_flop = step_flops_per_member(B) * P_local / n_step
@@ -347,7 +352,8 @@ def main():
                                 'cell_only_ms': round(float(np.mean([q['cell_only_ms'] for q in phases])), 3),
                                 'step_ms': round(ph['step_ms'], 3), 'logit_ms': round(ph['logit_ms'], 3),
                                 'cell_ms': round(ph['cell_ms'], 3),
-                                'shape': {'row_groups': G, 'slabs': nslabs, 'logit_split': S_split}}},
+                                'shape': {'row_groups': G, 'slabs': nslabs, 'logit_split': S_split},
+                                'path': path}},
         'cpu_baseline': cpu,
         'decodes_per_s': round(2 * value, 3),        # one decode = one sign's rollout of the batch
         'tie_fallbacks': eng.stats()['tie_fallbacks'],

@@ -213,7 +213,8 @@ int nicnes_kernel_times(nicnes_handle* h, float* out2_host);
  * kernel, [1] the two cell-only launches (t = -1, 0; one-launch-per-step builds only), [2] fused
  * path: the steps kernel (every step t = -1..T in one launch; or the per-step launches summed),
  * [3] its launch count, [4] split-path logit launches summed, [5] their count, [6] split-path cell
- * launches summed (token merge + next cell, t = -1..T), [7] their count. Synchronising. */
+ * launches summed (token merge + next cell, t = -1..T), [7] their count. The coop path's one launch
+ * counts as [2] / [3]. Synchronising. */
 int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host);
 
 /* Decode launch shape. Not a reference interface: the reference decodes one member per CPU process
@@ -231,6 +232,15 @@ int nicnes_decode_shape(nicnes_handle* h, int32_t B, int32_t count, int32_t* out
  * multi-stream decode records no per-launch events (nicnes_decode_phase_times reports zeros).
  * Tokens do not depend on n. */
 int nicnes_set_decode_streams(nicnes_handle* h, int32_t n);
+/* Coop decode (not a reference interface): when the split shape has 128-row slabs, S = 2 or 4 and every
+ * workgroup fits on the GPU at once (S x members x slabs <= CUs: 64 or 128 members per GPU at B = 128),
+ * the whole decode runs as one persistent launch whose S workgroups per member slab hand the partial
+ * greedy states and h' to each other (mode 1, the default; env NICNES_DECODE_COOP=0/1 sets the initial
+ * value), instead of two launches per step (mode 0). Tokens do not depend on it. */
+int nicnes_set_decode_coop(nicnes_handle* h, int32_t mode);
+/* the decode path an evaluate of `count` members of a B-image batch would take: 0 fused (one launch,
+ * one workgroup per member slab), 1 split (two launches per step), 2 coop (the split shape in one launch) */
+int nicnes_decode_path(nicnes_handle* h, int32_t B, int32_t count, int32_t* out_host);
 
 #ifdef __cplusplus
 }

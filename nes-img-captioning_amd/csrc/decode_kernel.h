@@ -2,6 +2,7 @@
 #pragma once
 #define SCR_SLOTS (64 + 64 + 64 + 1 + 64)   // per lane: c | h' | x of t = 0 | unfinished | h' (odd parity, split path)
 #define PART_FLOATS (8 * 7 * 64)             // split path: partial greedy state of one logit workgroup (8 waves x 7 x 64 lanes)
+#define COOP_CTR_STRIDE 32                   // coop path: uint32 per member-slab hand-off counter (its own 128-byte line)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -14,10 +15,12 @@ struct DecodeParams {
     int32_t* seq;                // out: [members, 2, B, T] greedy tokens (masked after the first 0)
     float* lp;                   // out (nullable): [members, 2, B, T] log-prob of the greedy token (nets.py:208,241)
     float* scratch;              // nicnes_decode_scratch_floats(): lane-private c | h' | x0 | unfinished | h' (odd)
-    int32_t* stats;              // [0] = exact-pass fallbacks (atomic)
+    int32_t* stats;              // [0] = exact-pass fallbacks (atomic), [2] = coop hand-off timeouts
     int32_t* alive;              // fused path: [members * slabs], 0 once every row of the workgroup finished
     int32_t* alive2;             // split path: [2][alive_stride] by step parity
     float* part;                 // split path: [members * slabs * S] x PART_FLOATS partial greedy states
+    uint32_t* coop_ctr;          // coop path: [members * slabs] x 32 hand-off counters (zeroed per launch)
+    int32_t coop;                // 1: the split shape (G = 4, S = 2 or 4) in one persistent launch
     int32_t force_exact;         // test hook (NICNES_FORCE_EXACT=1): every step takes the exact tie pass
     float lse_margin;            // widening of the bounded-lse interval: 2e-3 (test hook NICNES_LSE_MARGIN)
     int32_t bounded_lse;         // 1: greedy-only decode with the pair-bounded lse (needs lp == NULL)
@@ -35,6 +38,7 @@ struct DecodeParams {
 #define DK_STEPS 4       // fused path, every step in one launch (nicnes_decode_steps_kernel)
 #define DK_CELL 2        // split path: token merge of t + cell of t + 1
 #define DK_LOGIT 3       // split path: logits of t over one vocabulary range
+#define DK_COOP 5        // coop path: every step of the split shape in one launch
 
 // evs (nullable): up to DECODE_MAX_EVENTS events, recorded before the first launch and after every
 // launch; kinds[k] (k >= 1) is the kind of the launch that event k follows. Returns the launch count

@@ -1376,6 +1376,83 @@ __device__ __forceinline__ void load_part8(const DecodeParams& p, int wg, int wa
         }
 }
 
+// Merge of a row's nk = S * nh partial greedy states (split and coop paths): the merged (m, s) give the
+// tie window; the token is the first in-window record; ovf when a record is undecided (PAIRS) or an
+// evicted record is in the window (-> merge_exact). pre holds partials 0..7 (loaded by the caller).
+__device__ __forceinline__ void merge_partials(const DecodeParams& p, int wg, int wave, int lane, int nh, int nk,
+                                               const Part8& pre, bool pairs, float& m, float& lse, int& tok,
+                                               bool& ovf) {
+    float mh = -1.0e30f, sh = 0.f;
+    for (int k0 = 0; k0 < nk; k0 += 8) {              // every load of 8 partials issued before use
+        Part8 cur;
+        if (k0 == 0) cur = pre; else load_part8(p, wg, wave, lane, nh, nk, k0, cur);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (k0 + u < nk) {
+                const float mn = fmaxf(mh, cur.m[u]);
+                sh = sh * __builtin_amdgcn_exp2f((mh - mn) * LOG2E) + cur.s[u] * __builtin_amdgcn_exp2f((cur.m[u] - mn) * LOG2E);
+                mh = mn;
+            }
+    }
+    const float m_o = __shfl_xor(mh, 32);
+    const float s_o = __shfl_xor(sh, 32);
+    m = fmaxf(mh, m_o);
+    const float stot = sh * __builtin_amdgcn_exp2f((mh - m) * LOG2E) + s_o * __builtin_amdgcn_exp2f((m_o - m) * LOG2E);
+    const TieWindow w = tie_window(stot, pairs, p.lse_margin);
+    lse = w.lse;
+    for (int k0 = 0; k0 < nk; k0 += 8) {
+        Part8 cur;
+        if (k0 == 0) cur = pre; else load_part8(p, wg, wave, lane, nh, nk, k0, cur);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (k0 + u < nk) {
+                const int w0 = win_state(cur.r0v[u], m, w), w1 = win_state(cur.r1v[u], m, w);
+                if (w0 == 1 && cur.r0i[u] < tok) tok = cur.r0i[u];
+                if (w1 == 1 && cur.r1i[u] < tok) tok = cur.r1i[u];
+                ovf = ovf || w0 == 2 || w1 == 2 || win_state(cur.ev[u], m, w) != 0;
+            }
+    }
+    tok = min(tok, __shfl_xor(tok, 32));
+    ovf = ovf || (__shfl_xor(ovf ? 1 : 0, 32) != 0);
+}
+
+// rare: more records than tracked fall in the tie window, or (PAIRS mode) the bounds on lse leave a
+// record undecided -> exact pass over the whole vocabulary (every workgroup of the member does it: it
+// needs the token); PAIRS mode sums the exp first and re-decides from the records, sweeping for the
+// first id only when an evicted record is in the window. Workgroup-uniform call (barriers inside).
+__device__ __forceinline__ void merge_exact(const DecodeParams& p, float* lds, int wg, rsrc_t theta_r, rsrc_t noise_r,
+                                            int tid, int sgn, int hh, int wave, int lane, int nh, int nk,
+                                            const float (&hB)[64], bool folder, bool pairs, float m, float& lse,
+                                            int& tok) {
+    int best = 0x7fffffff;
+    float ssum = 0.f;
+    bool find = true;
+    if (pairs) {
+        exact_sweep(lds, p, theta_r, noise_r, tid, sgn, hh, lane, hB, folder, true, m, 0.f, ssum, best);
+        lse = logf(ssum + __shfl_xor(ssum, 32));
+        int t2 = 0x7fffffff;
+        bool ev2 = p.force_exact;
+        if (folder) {
+            for (int k = 0; k < nk; ++k) {
+                const float* pb = part_ptr(p, wg, k / nh, wave + k % nh) + lane;
+                const float r0v = pb[128], r1v = pb[256];
+                const int r0i = __builtin_bit_cast(int, pb[192]), r1i = __builtin_bit_cast(int, pb[320]);
+                if (in_window(r0v, m, lse) && r0i < t2) t2 = r0i;
+                if (in_window(r1v, m, lse) && r1i < t2) t2 = r1i;
+                ev2 = ev2 || in_window(pb[384], m, lse);
+            }
+            t2 = min(t2, __shfl_xor(t2, 32));
+            ev2 = ev2 || (__shfl_xor(ev2 ? 1 : 0, 32) != 0);
+        }
+        find = __syncthreads_or(ev2 ? 1 : 0) != 0;
+        if (!find) tok = t2;
+    }
+    if (find) {
+        exact_sweep(lds, p, theta_r, noise_r, tid, sgn, hh, lane, hB, folder, false, m, lse, ssum, best);
+        tok = min(best, __shfl_xor(best, 32));
+    }
+}
+
 template <int G>
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodeParams p, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1435,77 +1512,12 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
         int tok = 0x7fffffff;
         bool ovf = false;
         const bool pairs = p.bounded_lse && p.lp == nullptr;   // the logit kernel ran its PAIRS variant
-        TieWindow w = tie_window(1.f, false, 0.f);
-        if (folder) {
-            float mh = -1.0e30f, sh = 0.f;
-            for (int k0 = 0; k0 < nk; k0 += 8) {              // every load of 8 partials issued before use
-                Part8 cur;
-                if (k0 == 0) cur = pre; else load_part8(p, c.wg, c.wave, c.lane, nh, nk, k0, cur);
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (k0 + u < nk) {
-                        const float mn = fmaxf(mh, cur.m[u]);
-                        sh = sh * __builtin_amdgcn_exp2f((mh - mn) * LOG2E) + cur.s[u] * __builtin_amdgcn_exp2f((cur.m[u] - mn) * LOG2E);
-                        mh = mn;
-                    }
-            }
-            const float m_o = __shfl_xor(mh, 32);
-            const float s_o = __shfl_xor(sh, 32);
-            m = fmaxf(mh, m_o);
-            const float stot = sh * __builtin_amdgcn_exp2f((mh - m) * LOG2E) + s_o * __builtin_amdgcn_exp2f((m_o - m) * LOG2E);
-            w = tie_window(stot, pairs, p.lse_margin);
-            lse = w.lse;
-            for (int k0 = 0; k0 < nk; k0 += 8) {
-                Part8 cur;
-                if (k0 == 0) cur = pre; else load_part8(p, c.wg, c.wave, c.lane, nh, nk, k0, cur);
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (k0 + u < nk) {
-                        const int w0 = win_state(cur.r0v[u], m, w), w1 = win_state(cur.r1v[u], m, w);
-                        if (w0 == 1 && cur.r0i[u] < tok) tok = cur.r0i[u];
-                        if (w1 == 1 && cur.r1i[u] < tok) tok = cur.r1i[u];
-                        ovf = ovf || w0 == 2 || w1 == 2 || win_state(cur.ev[u], m, w) != 0;
-                    }
-            }
-            tok = min(tok, __shfl_xor(tok, 32));
-            ovf = ovf || (__shfl_xor(ovf ? 1 : 0, 32) != 0);
-        }
+        if (folder) merge_partials(p, c.wg, c.wave, c.lane, nh, nk, pre, pairs, m, lse, tok, ovf);
         PROF_SPLIT(pb0 + 10);
         load_h();
         if (__syncthreads_or((p.force_exact || ovf) ? 1 : 0)) {
-            // rare: more records than tracked fall in the tie window, or (PAIRS mode) the bounds on lse
-            // leave a record undecided -> exact pass over the whole vocabulary (every workgroup of the
-            // member does it: it needs the token); PAIRS mode sums the exp first and re-decides from the
-            // records, sweeping for the first id only when an evicted record is in the window
-            int best = 0x7fffffff;
-            float ssum = 0.f;
-            bool find = true;
-            if (pairs) {
-                exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, folder, true, m, 0.f,
-                            ssum, best);
-                lse = logf(ssum + __shfl_xor(ssum, 32));
-                int t2 = 0x7fffffff;
-                bool ev2 = p.force_exact;
-                if (folder) {
-                    for (int k = 0; k < nk; ++k) {
-                        const float* pb = part_ptr(p, c.wg, k / nh, c.wave + k % nh) + c.lane;
-                        const float r0v = pb[128], r1v = pb[256];
-                        const int r0i = __builtin_bit_cast(int, pb[192]), r1i = __builtin_bit_cast(int, pb[320]);
-                        if (in_window(r0v, m, lse) && r0i < t2) t2 = r0i;
-                        if (in_window(r1v, m, lse) && r1i < t2) t2 = r1i;
-                        ev2 = ev2 || in_window(pb[384], m, lse);
-                    }
-                    t2 = min(t2, __shfl_xor(t2, 32));
-                    ev2 = ev2 || (__shfl_xor(ev2 ? 1 : 0, 32) != 0);
-                }
-                find = __syncthreads_or(ev2 ? 1 : 0) != 0;
-                if (!find) tok = t2;
-            }
-            if (find) {
-                exact_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, folder, false, m, lse,
-                            ssum, best);
-                tok = min(best, __shfl_xor(best, 32));
-            }
+            merge_exact(p, lds, c.wg, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.wave, c.lane, nh, nk, hB, folder,
+                        pairs, m, lse, tok);
             if (lead) atomicAdd(p.stats + 0, 1);
         }
         if (tok >= p.V1) tok = 0;               // every logit NaN: end the caption (fused kernel rule)
@@ -1638,6 +1650,269 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
     PROF_SPLIT(pb0 + 11);
 }
 
+// ========== coop path: the split decode in ONE launch ==============================================
+// For populations too small to fill the chip with one workgroup per member slab (64 members per GPU:
+// configs[1], the per-GPU slice of configs[4] and of the metric at 8 GPUs; 128 at 4 GPUs), the S
+// workgroups of a member slab split the vocabulary as the split path does, but run every step in one
+// persistent launch and hand each other data inside it: per step t >= 1 the partial greedy states of
+// the logit ranges (phase A), then per step the unit blocks of h' (phase B). Every workgroup merges the
+// S partials into the same token (the tie rule holds on any partition of the vocabulary), runs the gate
+// tiles of its 4 / S unit blocks, and after phase B reads the whole h_{t+1} back for its logit range.
+// The logit W0 rows stay split over the XCDs as on the split path (workgroup L takes range q = L % S, and
+// blocks L, L + 8, ... share an XCD), and a phase's first staging tile is loaded during the previous
+// phase, as in the fused steps kernel.
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility; cdna_hip_programming.md Guideline 16, R1):
+// payload stored write-through (sc1) -> every storing wave s_waitcnt vmcnt(0) -> barrier -> one lane's
+// agent-scope atomic add on the group's counter; the consumer's wave 0 polls the counter relaxed, then
+// one agent acquire + vmcnt(0) + barrier before the plain loads. Counters are zeroed before each launch
+// (phase k complete = S * k arrivals). Residency: S * members * slabs <= CUs (checked on the host) and
+// one workgroup per CU (LDS), so a group's workgroups are resident together; every spin is bounded.
+#define COOP_SPIN_TICKS 50000000ull      // 0.5 s of s_memrealtime (100 MHz): a partner that never arrives
+
+__device__ __forceinline__ void st1_wt(rsrc_t r, uint32_t byte_off, uint32_t soff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)byte_off, (int)soff, 16);   // sc1
+}
+
+__device__ __forceinline__ void coop_arrive(uint32_t* ctr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // this wave's write-through stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// false (for every thread) when the partners have not arrived within COOP_SPIN_TICKS: the launch then
+// ends early and stats[2] counts it (the engine reports it as an error)
+__device__ __forceinline__ bool coop_wait(uint32_t* ctr, uint32_t target, int32_t* stats) {
+    int bad = 0;
+    if (threadIdx.x == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > COOP_SPIN_TICKS) {
+                bad = 1;
+                atomicAdd(stats + 2, 1);
+                break;
+            }
+        }
+    }
+    if (threadIdx.x < 64) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    return __syncthreads_or(bad) == 0;
+}
+
+// one step of one coop workgroup (range q of its member slab); false when the group is done (every
+// row finished, t = T, or a partner timed out). Mirrors step_body: s64 / pre carry a prefetched logit
+// tile across steps; hB holds h_t on entry (read back after the previous step's phase B).
+template <bool PAIRS, int S>
+__device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, int q, float* lds, int t,
+                                          Stage64Regs& s64, bool& pre, float (&hB)[64], uint32_t* ctr,
+                                          uint32_t& phase) {
+    const uint32_t lo = 4u * c.lane;
+    const int nst = (p.V1 + 63) >> 6;
+    const int s0 = q * nst / S, s1 = (q + 1) * nst / S;
+    // a range is never empty (nst >= S): without this the logit loop's zero-trip path changes the register
+    // allocation of the whole step (the cell loop spills its B operand)
+    __builtin_assume(s1 > s0);
+    const int nb = 4 / S, m0 = 5 * nb * q, m1 = m0 + 5 * nb;
+    const bool nl = t > 0;
+    const uint64_t nidx = p.noise_idx[c.member];
+    // the row's unfinished flag (every workgroup of the group writes the same value to the same slot)
+    const float unf_prev = nl ? ld1(c.scr_r, lo, U_SLOT) : 0.f;
+    if (t < 0) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) hB[i] = 0.f;               // h = 0 before the first cell
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) pin(hB[i]);
+    const uint32_t ib = (uint32_t)p.off_i2h_b, hb = (uint32_t)p.off_h2h_b, bmin = min(ib, hb);
+    auto csrc = [&](int m) {                                     // gate tile m: i2h rows | h2h rows
+        const uint32_t r = gate_row(m);
+        StageSrc Sx;
+        Sx.w_r = c.theta_r; Sx.z_r = c.noise_r; Sx.b_r = c.theta_r; Sx.bz_r = c.noise_r;
+        Sx.so_a = 4u * ((uint32_t)p.off_i2h_w + 128u * r);
+        Sx.so_b = 4u * ((uint32_t)p.off_h2h_w + 128u * r);
+        Sx.bso = 4u * (bmin + r);
+        Sx.bda = 4u * (ib - bmin); Sx.bdb = 4u * (hb - bmin);
+        Sx.valid = 64;
+        return Sx;
+    };
+    int it = 0;                                   // token fed to the next cell (0 = BOS at t = 0)
+    bool cell_pre = false;                        // s64 holds the cell's first gate tile
+    if (nl) {
+        RowState st;
+        row_state_init(st);
+        auto tail = [&]() __attribute__((always_inline)) {
+            if (CROSS_PREFETCH && t < p.T) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
+        };
+        logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, s0, s1, st, s64, pre && LOGIT_MIDSTORE, tail);
+        cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && t < p.T;
+        // ---- phase A: this range's partial greedy state, write-through, then the group's merge
+        {
+            const rsrc_t part_r = make_rsrc(part_ptr(p, c.wg, q, 0), PART_FLOATS * 4);
+            const uint32_t po = 4u * (uint32_t)(c.wave * (7 * 64) + lane_fresh());
+            st1_wt(part_r, po, 0u, st.m);
+            st1_wt(part_r, po, 256u, st.s);
+            st1_wt(part_r, po, 512u, st.r0v);
+            st1_wt(part_r, po, 768u, __builtin_bit_cast(float, st.r0i));
+            st1_wt(part_r, po, 1024u, st.r1v);
+            st1_wt(part_r, po, 1280u, __builtin_bit_cast(float, st.r1i));
+            st1_wt(part_r, po, 1536u, st.ev);
+        }
+        coop_arrive(ctr);
+        ++phase;
+        if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
+        float m = 0.f, lse = 0.f;
+        int tok = 0x7fffffff;
+        bool ovf = false;
+        {
+            Part8 pr;
+            load_part8(p, c.wg, c.wave, lane_fresh(), 1, S, 0, pr);
+            merge_partials(p, c.wg, c.wave, lane_fresh(), 1, S, pr, PAIRS, m, lse, tok, ovf);
+        }
+        if (__syncthreads_or((p.force_exact || ovf) ? 1 : 0)) {
+            // the exact sweep stages through LDS with registers of its own: the prefetched cell tile is
+            // given up (reloaded below)
+            merge_exact(p, lds, c.wg, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.wave, c.lane, 1, S, hB, true,
+                        PAIRS, m, lse, tok);
+            if (q == 0 && c.tid == 0) atomicAdd(p.stats + 0, 1);
+            cell_pre = false;
+        }
+        if (tok >= p.V1) tok = 0;               // every logit NaN: end the caption (fused kernel rule)
+        const bool unfinished = unf_prev != 0.f && tok > 0;
+        it = unfinished ? tok : 0;
+        st1(c.scr_r, lo, U_SLOT, unfinished ? 1.f : 0.f);
+        if (q == 0 && c.hh == 0 && c.row_valid) {
+            const size_t o = (((size_t)c.member * 2 + c.sgn) * p.B + c.b) * p.T + (t - 1);
+            p.seq[o] = it;
+            if (p.lp) p.lp[o] = -lse;           // seq_logprobs[:, t-1] (nets.py:208,241)
+        }
+        // every workgroup of the group reaches the same decision (the reference stops here, nets.py:242-243)
+        if (!__syncthreads_or((unfinished && c.row_valid) ? 1 : 0)) return false;
+    }
+    if (t >= p.T) return false;
+
+    // ---- LSTM cell of step t+1, gate tiles of this workgroup's unit blocks (nets.py:98-134) ---------
+    float xB[64];
+    if (t < 0) {                                                 // x = img_embed(fc) (nets.py:194-195)
+#pragma unroll
+        for (int i = 0; i < 64; ++i) xB[i] = ld1(c.scr_r, lo, X_SLOT(i));
+    } else {                                                     // x = embed(it) (nets.py:196-199)
+        const uint32_t eo = 4u * ((uint32_t)p.off_emb_w + (uint32_t)it * 128u + 4u * c.hh);
+#pragma unroll
+        for (int T = 0; T < 4; ++T)
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const f32x4 w = ld4(c.theta_r, eo + 4u * (32 * T + 8 * a));
+                const f32x4 z = ld4(c.noise_r, eo + 4u * (32 * T + 8 * a));
+                const f32x4 x = c.sgn ? (w - z) : (w + z);         // the table is sigma-scaled
+#pragma unroll
+                for (int e = 0; e < 4; ++e) xB[16 * T + 4 * a + e] = x[e];
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) pin(xB[i]);
+    const int hpar = (t + 1) & 1;
+    if (!cell_pre) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
+    stage64_store(lds, 64, c.wave * 64 + lane_fresh(), s64);
+    __syncthreads();
+    f32x16 hold;
+    auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) __attribute__((always_inline)) {
+        const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
+        const int U = m / 5, j5 = m % 5;
+        if (j5 == 0) {                                           // g1
+            hold = s_;
+        } else if (j5 == 1) {                                    // g = max(g1, g2)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hold[r] = hold[r] > s_[r] ? hold[r] : s_[r];
+        } else if (j5 == 2) {                                    // ig * g
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hold[r] = CELL_SIG(s_[r]) * hold[r];
+        } else if (j5 == 3) {                                    // c' = f * c + ig * g
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float fcv = CELL_SIG(s_[r]) * cpre[r];
+                const float cn = fcv + hold[r];
+                st1(c.scr_r, lo_, C_SLOT(16 * U + r), cn);      // c: read back only by this workgroup
+                hold[r] = cn;
+            }
+        } else {                                                 // h' = o * tanh(c'), handed to the group
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                st1_wt(c.scr_r, lo_, HP_SLOT(hpar, 16 * U + r), CELL_SIG(s_[r]) * CELL_TANH(hold[r]));
+        }
+    };
+    auto load_c = [&](int m) __attribute__((always_inline)) {   // c of the f tile's unit block
+        f32x16 cp;
+        const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cp[r] = (m % 5 == 3 && t >= 0) ? ld1(c.scr_r, lo_, C_SLOT(16 * (m / 5) + r)) : 0.f;
+        return cp;
+    };
+    const bool lpf = LOGIT_MIDSTORE && CROSS_PREFETCH && t >= 0;   // the next step's first logit tile
+#pragma unroll 1
+    for (int m = m0; m < m1; ++m) {
+        const f32x16 cpre = load_c(m);
+        __builtin_amdgcn_sched_barrier(0);
+        if (m + 1 < m1) {
+            stage64_load(csrc(m + 1), c.wave * 64 + lane_fresh(), s64);
+        } else if (lpf) {
+            const LaneOffs lo_ = lane_offs(c.wave, 128u);
+            stage64_load_o(logit_src(p, nidx, s0), lo_, c.wave < 2, s64);
+        }
+        const float* buf = lds + ((m - m0) & 1) * STAGE64_FLOATS;
+        f32x16 a0, a1;
+        if (t < 0)      // h = 0 before the first cell: h2h(h) is its bias (fma(w, 0, acc) == acc)
+            mfma_xh_part<0, 4, false>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
+        else
+            mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
+        fold(m, a0 + a1, cpre);                                  // i2h(x) + h2h(h), nets.py:109-111
+        if (m + 1 < m1) stage64_store(lds + ((m - m0 + 1) & 1) * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
+        __syncthreads();
+    }
+    pre = lpf;
+    // ---- phase B: h_{t+1} complete in the group -> every workgroup reads all of it
+    coop_arrive(ctr);
+    ++phase;
+    if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, HP_SLOT(hpar, i));
+    return true;
+}
+
+// grid: S x member slabs workgroups, L = blockIdx.x -> range q = L % S of group L / S
+template <bool PAIRS, int S>
+__global__ __launch_bounds__(NTHREADS) void nicnes_decode_coop_kernel(DecodeParams p, int nslabs) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int L = blockIdx.x, q = L % S, gi = L / S;
+    Ctx c;
+    c.tid = threadIdx.x;
+    c.lane = c.tid & 63;
+    c.wave = __builtin_amdgcn_readfirstlane(c.tid >> 6);
+    c.sgn = c.wave >> 2;
+    c.grp = c.wave & 3;
+    c.hh = c.lane >> 5;
+    c.member = gi / nslabs;
+    c.slab = gi % nslabs;
+    c.wg = gi;
+    c.b = c.slab * 128 + c.grp * 32 + (c.lane & 31);
+    c.row_valid = c.b < p.B;
+    c.bc = c.row_valid ? c.b : 0;
+    const uint64_t nidx = p.noise_idx[c.member];
+    const uint32_t Dbytes = 4u * (uint32_t)p.D;
+    c.theta_r = make_rsrc(p.theta, Dbytes);
+    c.noise_r = make_rsrc(p.noise + nidx, Dbytes);
+    float* wscr = p.scratch + ((size_t)c.wg * 8 + c.wave) * (SCR_SLOTS * 64);
+    c.scr_r = make_rsrc(wscr, SCR_SLOTS * 64 * 4);
+    uint32_t* ctr = p.coop_ctr + (size_t)gi * COOP_CTR_STRIDE;
+    uint32_t phase = 0;
+    Stage64Regs s64;
+    bool pre = false;
+    float hB[64];
+    for (int t = -1; t <= p.T; ++t)
+        if (!coop_step<PAIRS, S>(p, c, q, lds, t, s64, pre, hB, ctr, phase)) break;
+}
+
 namespace {
 const size_t LDS64 = (size_t)(2 * STAGE64_FLOATS) * sizeof(float);
 const size_t LDS32 = (size_t)(2 * STAGE_FLOATS) * sizeof(float);
@@ -1657,6 +1932,10 @@ extern "C" hipError_t nicnes_decode_init() {
         {(const void*)nicnes_decode_logit_kernel<2, true>, LDS64},
         {(const void*)nicnes_decode_logit_kernel<2, false>, LDS64},
         {(const void*)nicnes_decode_cell_kernel<4>, LDS64},
+        {(const void*)nicnes_decode_coop_kernel<true, 2>, LDS64},
+        {(const void*)nicnes_decode_coop_kernel<false, 2>, LDS64},
+        {(const void*)nicnes_decode_coop_kernel<true, 4>, LDS64},
+        {(const void*)nicnes_decode_coop_kernel<false, 4>, LDS64},
         {(const void*)nicnes_decode_cell_kernel<2>, LDS_CELL2},
         {(const void*)nicnes_decode_img_kernel<4>, LDS32},
         {(const void*)nicnes_decode_img_kernel<2>, LDS32},
@@ -1679,6 +1958,7 @@ extern "C" void nicnes_decode_shift(DecodeParams* p, int m0, int nslabs) {
     p->alive += wg0;
     p->alive2 += wg0;
     p->part += wg0 * (size_t)p->S * PART_FLOATS;                 // part_ptr
+    if (p->coop_ctr) p->coop_ctr += wg0 * COOP_CTR_STRIDE;
 }
 
 extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,
@@ -1686,7 +1966,8 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
     const bool fused = p->G == 4 && p->S == 1;
     if (p->G != 4 && p->G != 2) return hipErrorInvalidValue;
     if (p->S < 1 || p->S > 64) return hipErrorInvalidValue;
-    const int nl = fused ? p->T + 3 : 3 + 2 * p->T;
+    if (p->coop && (p->G != 4 || (p->S != 2 && p->S != 4) || !p->coop_ctr)) return hipErrorInvalidValue;
+    const int nl = fused || p->coop ? p->T + 3 : 3 + 2 * p->T;
     if (evs && nl + 1 > DECODE_MAX_EVENTS) return hipErrorInvalidValue;
     int ne = 0;
     auto mark = [&](int kind) {
@@ -1700,7 +1981,27 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
     // nicnes_evaluate_batches); with p->lp the exact exp-sum gives seq_logprobs
     const bool pairs = p->bounded_lse && p->lp == nullptr;
     mark(0);
-    if (fused) {
+    if (p->coop) {
+        // the group counters are zeroed before every launch (one 128-byte line per member slab)
+        hipError_t e = hipMemsetAsync(p->coop_ctr, 0, (size_t)member_count * nslabs * COOP_CTR_STRIDE * sizeof(uint32_t),
+                                      stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(p->S, member_count, nslabs), block, LDS32, stream, *p);
+        mark(DK_IMG);
+        const dim3 grid(p->S * member_count * nslabs);
+        if (p->S == 2) {
+            if (pairs)
+                hipLaunchKernelGGL((nicnes_decode_coop_kernel<true, 2>), grid, block, LDS64, stream, *p, nslabs);
+            else
+                hipLaunchKernelGGL((nicnes_decode_coop_kernel<false, 2>), grid, block, LDS64, stream, *p, nslabs);
+        } else {
+            if (pairs)
+                hipLaunchKernelGGL((nicnes_decode_coop_kernel<true, 4>), grid, block, LDS64, stream, *p, nslabs);
+            else
+                hipLaunchKernelGGL((nicnes_decode_coop_kernel<false, 4>), grid, block, LDS64, stream, *p, nslabs);
+        }
+        mark(DK_COOP);
+    } else if (fused) {
         if (IMG64)
             hipLaunchKernelGGL(nicnes_decode_img64_kernel, dim3(member_count, nslabs), block, LDS64, stream, *p);
         else

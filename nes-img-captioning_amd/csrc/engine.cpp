@@ -104,6 +104,8 @@ struct nicnes_handle {
     // 0 = automatic: 2 on the split path, 1 on the fused path): one part's launches fill the CUs the
     // others' launch gaps and tails leave idle
     int dec_streams = 0;
+    int coop_mode = 1;                // nicnes_set_decode_coop: 0 never, 1 the split shape in one launch when it fits
+    uint32_t* coop_ctr = nullptr;     // [max_members * slabs * COOP_CTR_STRIDE] coop hand-off counters
     hipStream_t sx[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_fork = nullptr;
     hipEvent_t ev_join[3] = {nullptr, nullptr, nullptr};
@@ -215,6 +217,12 @@ void decode_shape(const nicnes_handle* h, int B, int count, int* G, int* nslabs,
     *S = h->dec_S ? h->dec_S : auto_split((int64_t)count * *nslabs, h->n_cu, *G);
 }
 
+// The coop path (the split shape in one persistent launch, nicnes_decode_coop_kernel): 128-row slabs, 2 or
+// 4 logit ranges per member slab, and every workgroup of the launch resident at once (one per CU).
+bool coop_fits(const nicnes_handle* h, int G, int nslabs, int S, int count) {
+    return h->coop_mode && G == 4 && (S == 2 || S == 4) && (int64_t)count * nslabs * S <= h->n_cu;
+}
+
 // Buffers sized by the reference count: the cooked reference n-gram vectors (CIDEr-D).
 int alloc_refs(nicnes_handle* h, int max_refs) {
     void* old[] = {h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2, h->ref_norm};
@@ -239,6 +247,8 @@ int alloc_batch(nicnes_handle* h, int max_batch) {
         if (q) (void)hipFree(q);
     h->seq = nullptr; h->lp = nullptr; h->row_scores = nullptr; h->dscratch = nullptr; h->alive = nullptr;
     h->part = nullptr;
+    if (h->coop_ctr) (void)hipFree(h->coop_ctr);
+    h->coop_ctr = nullptr;
     const size_t MM = (size_t)h->cfg.max_members, MB = (size_t)max_batch, T = (size_t)h->cfg.seq_length;
     // lane scratch: 2G row waves per slab, the larger of the two slab layouts
     const int rw = std::max(8 * nslabs_of((int)MB, 4), 4 * nslabs_of((int)MB, 2));
@@ -249,6 +259,7 @@ int alloc_batch(nicnes_handle* h, int max_batch) {
     if (!rc) rc = dalloc(h, &h->lp, MM * 2 * MB * T);
     if (!rc) rc = dalloc(h, &h->row_scores, MM * 2 * MB);
     if (!rc) rc = dalloc(h, &h->dscratch, nicnes_decode_scratch_floats((int)MM, rw));
+    if (!rc) rc = dalloc(h, &h->coop_ctr, MM * (size_t)ns * COOP_CTR_STRIDE);
     if (!rc) rc = dalloc(h, &h->alive, 3 * (size_t)h->alive_stride);
     if (!rc) rc = dalloc(h, &h->part, (size_t)h->part_cap * PART_FLOATS);
     if (!rc) h->cfg.max_batch = max_batch;
@@ -330,6 +341,8 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
         if (bl && (bl[0] == '0' || bl[0] == '1')) h->bounded_mode = bl[0] - '0';
         const char* ds = getenv("NICNES_DECODE_STREAMS");
         if (ds && ds[0] >= '1' && ds[0] <= '4' && ds[1] == 0) h->dec_streams = ds[0] - '0';
+        const char* dc = getenv("NICNES_DECODE_COOP");
+        if (dc && (dc[0] == '0' || dc[0] == '1') && dc[1] == 0) h->coop_mode = dc[0] - '0';
     }
     {
         int ncu = 0;
@@ -381,7 +394,7 @@ int nicnes_destroy(nicnes_handle* h) {
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
                     h->ref_norm, h->nidx, h->seq, h->lp, h->row_scores, h->dscratch, h->stats, h->partials, h->norms,
                     h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive, h->part,
-                    h->rank_key, h->rank_idx, h->mbatch, h->mut_vec, h->dbuf, h->didx, h->noise_sc};
+                    h->rank_key, h->rank_idx, h->mbatch, h->mut_vec, h->dbuf, h->didx, h->noise_sc, h->coop_ctr};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (h->stats_pending) (void)hipEventSynchronize(h->stats_ev);
@@ -702,6 +715,8 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     p.lse_margin = h->lse_margin;
     if (h->stats_pending && hipEventQuery(h->stats_ev) == hipSuccess) {   // the last decode's fallbacks
         const int32_t fb = h->stats_host[0];
+        if (h->stats_host[2] != 0)
+            return fail(h, NICNES_ERR_HIP, "coop decode: a workgroup's partners never arrived (hand-off timeout)");
         if (h->last_bounded && fb - h->fb_seen >= 2) h->exact_left = 32;
         h->fb_seen = fb;
         h->stats_pending = false;
@@ -716,6 +731,8 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     p.G = G;
     p.S = S;
     p.part = h->part;
+    p.coop = coop_fits(h, G, nslabs, S, count) ? 1 : 0;
+    p.coop_ctr = h->coop_ctr;
     p.alive2 = h->alive + h->alive_stride;
     p.alive_stride = h->alive_stride;
     p.B = h->B;
@@ -737,7 +754,8 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     if (p.lp) HIPC(h, hipMemsetAsync(p.lp, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(float), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
     int n_ev = 0;
-    const int nstr = std::min(count, h->dec_streams ? h->dec_streams : ((G == 4 && S == 1) ? 1 : 2));
+    // the coop launch needs all its workgroups resident: never split over streams
+    const int nstr = p.coop ? 1 : std::min(count, h->dec_streams ? h->dec_streams : ((G == 4 && S == 1) ? 1 : 2));
     if (nstr > 1) {
         // members split evenly over the caller's stream and nstr - 1 engine streams; the parts share
         // nothing but the fallback counter (an atomic). No per-launch events: the launches overlap
@@ -946,6 +964,7 @@ int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host) {
                 if (n_cell_only < 2) { o[1] += ms; ++n_cell_only; }
                 break;
             case DK_STEPS: o[2] += ms; o[3] += 1; break;      // every step in one launch
+            case DK_COOP: o[2] += ms; o[3] += 1; break;       // the split shape, every step in one launch
             case DK_LOGIT: o[4] += ms; o[5] += 1; break;
             default:
                 o[6] += ms; o[7] += 1;
@@ -960,6 +979,20 @@ int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host) {
 int nicnes_set_decode_streams(nicnes_handle* h, int32_t n) {
     if (!h || n < 0 || n > 4) return NICNES_ERR_INVALID;
     h->dec_streams = n;
+    return NICNES_OK;
+}
+
+int nicnes_set_decode_coop(nicnes_handle* h, int32_t mode) {
+    if (!h || (mode != 0 && mode != 1)) return NICNES_ERR_INVALID;
+    h->coop_mode = mode;
+    return NICNES_OK;
+}
+
+int nicnes_decode_path(nicnes_handle* h, int32_t B, int32_t count, int32_t* out_host) {
+    if (!h || !out_host || B < 1 || count < 1) return NICNES_ERR_INVALID;
+    int G = 0, nslabs = 0, S = 0;
+    decode_shape(h, B, count, &G, &nslabs, &S);
+    *out_host = (G == 4 && S == 1) ? 0 : coop_fits(h, G, nslabs, S, count) ? 2 : 1;
     return NICNES_OK;
 }
 

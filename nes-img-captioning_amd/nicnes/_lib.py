@@ -19,7 +19,8 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_optimizer_update', 'nicnes_last_ratio', 'nicnes_set_fitness_mode', 'nicnes_evaluate_lp',
            'nicnes_set_decode_split', 'nicnes_decode_shape', 'nicnes_set_decode_streams', 'nicnes_comm_unique_id', 'nicnes_comm_init',
            'nicnes_comm_attach', 'nicnes_comm_destroy', 'nicnes_allgather_fitness', 'nicnes_allreduce_grad',
-           'nicnes_noise_vectors', 'nicnes_set_batches', 'nicnes_evaluate_batches', 'nicnes_set_mutation']
+           'nicnes_noise_vectors', 'nicnes_set_batches', 'nicnes_evaluate_batches', 'nicnes_set_mutation',
+           'nicnes_set_decode_coop', 'nicnes_decode_path']
 
 
 class NicnesConfig(ctypes.Structure):
@@ -79,6 +80,8 @@ def lib(path=None):
         'nicnes_set_decode_split': (c.c_int, [vp, i32, i32]),
         'nicnes_decode_shape': (c.c_int, [vp, i32, i32, vp]),
         'nicnes_set_decode_streams': (c.c_int, [vp, i32]),
+        'nicnes_set_decode_coop': (c.c_int, [vp, i32]),
+        'nicnes_decode_path': (c.c_int, [vp, i32, i32, vp]),
         'nicnes_comm_unique_id': (c.c_int, [vp]),
         'nicnes_comm_init': (c.c_int, [vp, i32, i32, vp]),
         'nicnes_comm_attach': (c.c_int, [vp, vp]),

@@ -4,6 +4,7 @@ PyTorch-ROCm tensors are used for device storage only (their data_ptr() goes thr
 all arithmetic of the path runs in the HIP kernels of libnicnes.so.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -58,6 +59,7 @@ class Engine:
             check(self.L.nicnes_create(ctypes.byref(self.cfg), device, ctypes.byref(h)), None, 'nicnes_create')
         self.h = h
         self.n_cu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        self.coop_mode = 0 if os.environ.get('NICNES_DECODE_COOP') == '0' else 1
         self._keep = {}
         self.B = 0
 
@@ -311,6 +313,19 @@ class Engine:
         Tokens do not depend on it."""
         check(self.L.nicnes_set_decode_streams(self.h, int(n)), self.h, 'set_decode_streams')
 
+    def set_decode_coop(self, mode=1):
+        """1 (default): the split shape (128-row slabs, S = 2 or 4, every workgroup resident) runs as one
+        persistent launch whose workgroups hand partial states and h' to each other; 0: two launches per
+        step. Tokens do not depend on it."""
+        check(self.L.nicnes_set_decode_coop(self.h, int(mode)), self.h, 'set_decode_coop')
+        self.coop_mode = int(mode)
+
+    def decode_path(self, B=None, count=1):
+        """'fused', 'split' or 'coop': the decode path an evaluate of `count` members would take."""
+        out = ctypes.c_int32()
+        check(self.L.nicnes_decode_path(self.h, int(B or self.B), int(count), ctypes.byref(out)), self.h, 'decode_path')
+        return ('fused', 'split', 'coop')[out.value]
+
     def decode_shape(self, B=None, count=1):
         """(G, slabs, S) an evaluate of `count` members would use."""
         out = (ctypes.c_int32 * 3)()
@@ -352,4 +367,4 @@ class Engine:
     def stats(self):
         out = (ctypes.c_int64 * 4)()
         check(self.L.nicnes_stats(self.h, out), self.h, 'stats')
-        return {'tie_fallbacks': out[0]}
+        return {'tie_fallbacks': out[0], 'coop_timeouts': out[2]}

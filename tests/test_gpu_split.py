@@ -1,6 +1,8 @@
 """GPU parity of the split decode path (nicnes_decode_logit_kernel / nicnes_decode_cell_kernel):
 one member's step spread over S workgroups (vocabulary ranges for the logits, unit blocks for the
-cell) and 64-row slabs (G = 2) for batches of <= 64 images, against the C oracle.
+cell) and 64-row slabs (G = 2) for batches of <= 64 images, against the C oracle. Every test runs
+twice: with the coop path on (nicnes_decode_coop_kernel takes the G = 4, S = 2 / 4 shapes in one
+launch) and off (two launches per step for every split shape).
 
 Covers the shapes the automatic rule picks for BASELINE.json configs[1] (pop=64, B=128 -> S=4) and
 mscoco_nes.json's batch_size 64 (G=2), forced shapes from the fused kernel (G=4, S=1) up to S=16,
@@ -22,15 +24,17 @@ SIGMA = 0.01
 SHAPES = [(4, 1), (4, 2), (4, 4), (4, 16), (2, 1), (2, 4), (2, 8)]
 
 
-@pytest.fixture(scope='module')
-def eng():
+@pytest.fixture(scope='module', params=[1, 0], ids=['coop', 'nocoop'])
+def eng(request):
     import nicnes
     assert torch.cuda.is_available(), 'GPU tests need a GPU'
     e = nicnes.Engine(max_batch=128, max_members=64, noise_len=NOISE_LEN, noise_seed=5)
     table = O.noise_table(NOISE_LEN, 123)
     e.set_noise_table(table)
     e._table_np = table
+    e.set_decode_coop(request.param)
     yield e
+    assert e.stats()['coop_timeouts'] == 0
     e.set_decode_split(0, 0)
     e.close()
 
@@ -116,6 +120,7 @@ def test_pop64_auto_shape_tokens_and_fitness(eng, B, want):
     shape = eng.decode_shape(B, P)
     if eng.n_cu == 256:
         assert shape == want
+        assert eng.decode_path(B, P) == ('coop' if (B == 128 and eng.coop_mode) else 'split')
     fit, seq = eng.evaluate(1, 0, P, SIGMA, return_seq=True)
     fit, seq = fit.cpu().numpy(), seq.cpu().numpy()
     idx = eng.noise_indices(1, 0, P).cpu().numpy()
@@ -178,12 +183,14 @@ def test_early_exit_matches_oracle(eng, G, S, bias0):
         assert np.abs(lp - olp).max() <= 1e-5              # zeros past the global exit, as the reference
 
 
-def test_split_exact_tie_pass_matches_oracle(monkeypatch):
+@pytest.mark.parametrize('coop', [1, 0], ids=['coop', 'nocoop'])
+def test_split_exact_tie_pass_matches_oracle(monkeypatch, coop):
     """The exact second pass forced on every step of the split path (every cell workgroup of a
     member runs it): tokens still match the oracle."""
     import nicnes
     monkeypatch.setenv('NICNES_FORCE_EXACT', '1')
     e = nicnes.Engine(max_batch=64, max_members=2, noise_len=NOISE_LEN, noise_seed=7)
+    e.set_decode_coop(coop)
     try:
         table = O.noise_table(NOISE_LEN, 123)
         e.set_noise_table(table)
