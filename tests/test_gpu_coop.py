@@ -73,12 +73,15 @@ def test_decode_path_rule(eng):
     assert eng.decode_path(128, 128) == 'coop' and eng.decode_shape(128, 128) == (4, 1, 2)
     assert eng.decode_path(128, 256) == 'fused' and eng.decode_path(128, 512) == 'fused'
     assert eng.decode_path(64, 64) == 'split'                  # 64-row slabs stay on the two-launch path
-    assert eng.decode_path(130, 64) == 'coop' and eng.decode_shape(130, 64) == (4, 2, 2)
-    eng.set_decode_coop(0)
+    assert eng.decode_path(130, 64) == 'split'                 # B = 130 pads least with 64-row slabs
+    eng.set_decode_split(0, 4)                                # forced 128-row slabs: two of them
     try:
+        assert eng.decode_path(130, 64) == 'coop' and eng.decode_shape(130, 64) == (4, 2, 2)
+        eng.set_decode_coop(0)
         assert eng.decode_path(128, 64) == 'split'
     finally:
         eng.set_decode_coop(1)
+        eng.set_decode_split(0, 0)
 
 
 @pytest.mark.parametrize('B,P', [(128, 64), (128, 128), (130, 64), (100, 3)],
@@ -90,6 +93,8 @@ def test_coop_equals_split_and_oracle(eng, B, P):
     _load(eng, theta, fc)
     if P < 8:
         eng.set_decode_split(4, 4)                # a few members: the automatic rule would split wider
+    elif B > 128:
+        eng.set_decode_split(0, 4)                # two 128-row slabs (the automatic rule takes 64-row ones)
     try:
         assert eng.decode_path(B, P) == 'coop'
         fit_c, seq_c, lp_c = eng.evaluate(4, 5, P, SIGMA, return_seq=True, return_lp=True)
