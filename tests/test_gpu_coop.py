@@ -182,12 +182,24 @@ def test_coop_exact_pass_and_undecided_rows(monkeypatch):
         monkeypatch.delenv(env)
 
 
-def test_coop_repeated_launches_are_deterministic(eng):
+@pytest.mark.parametrize('bounded', ['1', '0'], ids=['bounded_lse', 'exact_sum'])
+def test_coop_repeated_launches_are_deterministic(monkeypatch, bounded):
     """back-to-back coop launches (counters re-zeroed per launch, uneven progress between groups):
-    identical results every time"""
-    dims = O.Dims()
-    _load(eng, O.make_theta(dims, 2, 4.0, 0.1), _fc(128, 8))
-    ref = eng.evaluate(7, 0, 64, SIGMA, return_seq=True)
-    for _ in range(5):
-        got = eng.evaluate(7, 0, 64, SIGMA, return_seq=True)
-        assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+    identical results every time. The lse mode is pinned (NICNES_BOUNDED_LSE): the adaptive policy
+    may switch a decode to the exact exp-sum, whose tokens may differ from the bounded one's at
+    lse-fragile steps (both equal the reference's up to such a step)."""
+    monkeypatch.setenv('NICNES_BOUNDED_LSE', bounded)
+    e = _engine(max_batch=128, max_members=64)
+    try:
+        dims = O.Dims()
+        _load(e, O.make_theta(dims, 2, 4.0, 0.1), _fc(128, 8))
+        assert e.decode_path(128, 64) == 'coop' or e.n_cu != 256
+        ref = [x.clone() for x in e.evaluate(7, 0, 64, SIGMA, return_seq=True)]
+        for it in range(5):
+            got = e.evaluate(7, 0, 64, SIGMA, return_seq=True)
+            bad = (got[1] != ref[1]).nonzero()
+            assert bad.shape[0] == 0, (it, bad[:8].tolist(), e.stats())
+            assert torch.equal(got[0], ref[0])
+        assert e.stats()['coop_timeouts'] == 0
+    finally:
+        e.close()
