@@ -21,6 +21,7 @@ struct DecodeParams {
     float* part;                 // split path: [members * slabs * S] x PART_FLOATS partial greedy states
     uint32_t* coop_ctr;          // coop path: [members * slabs] x 32 hand-off counters (zeroed per launch)
     int32_t coop;                // 1: the split shape (G = 4, S = 2 or 4) in one persistent launch
+    int32_t no_exit;             // 1: no per-slab early exit (log-probs of a multi-slab batch, see below)
     int32_t force_exact;         // test hook (NICNES_FORCE_EXACT=1): every step takes the exact tie pass
     float lse_margin;            // widening of the bounded-lse interval: 2e-3 (test hook NICNES_LSE_MARGIN)
     int32_t bounded_lse;         // 1: greedy-only decode with the pair-bounded lse (needs lp == NULL)
@@ -50,5 +51,9 @@ extern "C" hipError_t nicnes_decode_init();
 extern "C" void nicnes_decode_shift(DecodeParams* p, int m0, int nslabs);
 extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,
                                            hipEvent_t* evs, int* kinds, int* n_launch);
+// zero seq_logprobs past the batch's last finishing step (rollouts = members x 2 of B rows; after a
+// no_exit decode of a batch spanning several slabs)
+extern "C" hipError_t nicnes_launch_lp_batch_exit(const int32_t* seq, float* lp, int rollouts, int B, int T,
+                                                  hipStream_t stream);
 // lane scratch for up to member_count members x row_waves 32-row waves of one sign
 extern "C" size_t nicnes_decode_scratch_floats(int member_count, int row_waves_per_member);

@@ -46,7 +46,7 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef DECODE_ABLATE
 #define DECODE_ABLATE 0    // timing-only builds (scripts/ablate.py): 1 no logit epilogue, 4 no exp-sum, 2 no stage
 #endif                     // staging, 8 no stage-loop barrier, 16 no cell activations, 64 no early
-                           // exit -- wrong results
+                           // exit, 128 no coop hand-off waits -- wrong results
 #if DECODE_ABLATE & 16
 #define CELL_SIG(x) ((x) * 0.5f)
 #define CELL_TANH(x) ((x) * 0.25f)
@@ -108,6 +108,7 @@ __device__ __forceinline__ void wave_prio(int wave) {
 #define PROF_MARK(slot) PROF_AT(blockIdx.x * gridDim.y + blockIdx.y, 4096, slot)
 #define PROF_SPLIT(slot) PROF_AT((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, 1024, slot)
 #else
+#define PROF_AT(wgi, stride, slot) do { } while (0)
 #define PROF_MARK(slot) do { } while (0)
 #define PROF_SPLIT(slot) do { } while (0)
 #endif
@@ -1180,7 +1181,7 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
             if (p.lp) p.lp[o] = -lse;
         }
 #endif
-        const int any = __syncthreads_or(((unfinished && c.row_valid) || (DECODE_ABLATE & 64)) ? 1 : 0);
+        const int any = __syncthreads_or(((unfinished && c.row_valid) || p.no_exit || (DECODE_ABLATE & 64)) ? 1 : 0);
         if (c.tid == 0) p.alive[c.wg] = any;
         if (!any) { PROF_MARK(2 * (t + 1) + 1); return false; } // the reference stops here (nets.py:242-243)
     }
@@ -1535,7 +1536,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
             if (p.lp) p.lp[o] = -lse;           // seq_logprobs[:, t-1] (nets.py:208,241)
         }
 #endif
-        const int any = __syncthreads_or((folder && unfinished && c.row_valid) ? 1 : 0);
+        const int any = __syncthreads_or(((folder && unfinished && c.row_valid) || p.no_exit) ? 1 : 0);
         if (lead) p.alive2[(t & 1) * p.alive_stride + c.wg] = any;
         if (!any) return;                       // the reference stops here (nets.py:242-243)
         PROF_SPLIT(pb0 + 1);
@@ -1708,6 +1709,8 @@ template <bool PAIRS, int S>
 __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, int q, float* lds, int t,
                                           Stage64Regs& s64, bool& pre, float (&hB)[64], uint32_t* ctr,
                                           uint32_t& phase) {
+    [[maybe_unused]] const int pm = 8 * (t + 1);         // DECODE_PROF slots: start, logits, A, token, cell, B
+    PROF_AT(blockIdx.x, 1024, pm);
     const uint32_t lo = 4u * c.lane;
     const int nst = (p.V1 + 63) >> 6;
     const int s0 = q * nst / S, s1 = (q + 1) * nst / S;
@@ -1747,6 +1750,7 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         };
         logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, s0, s1, st, s64, pre && LOGIT_MIDSTORE, tail);
         cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && t < p.T;
+        PROF_AT(blockIdx.x, 1024, pm + 1);
         // ---- phase A: this range's partial greedy state, write-through, then the group's merge
         {
             const rsrc_t part_r = make_rsrc(part_ptr(p, c.wg, q, 0), PART_FLOATS * 4);
@@ -1761,7 +1765,10 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         }
         coop_arrive(ctr);
         ++phase;
+#if !(DECODE_ABLATE & 128)
         if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
+#endif
+        PROF_AT(blockIdx.x, 1024, pm + 2);
         float m = 0.f, lse = 0.f;
         int tok = 0x7fffffff;
         bool ovf = false;
@@ -1782,13 +1789,16 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         const bool unfinished = unf_prev != 0.f && tok > 0;
         it = unfinished ? tok : 0;
         st1(c.scr_r, lo, U_SLOT, unfinished ? 1.f : 0.f);
+#if !DECODE_PROF
         if (q == 0 && c.hh == 0 && c.row_valid) {
             const size_t o = (((size_t)c.member * 2 + c.sgn) * p.B + c.b) * p.T + (t - 1);
             p.seq[o] = it;
             if (p.lp) p.lp[o] = -lse;           // seq_logprobs[:, t-1] (nets.py:208,241)
         }
+#endif
+        PROF_AT(blockIdx.x, 1024, pm + 3);
         // every workgroup of the group reaches the same decision (the reference stops here, nets.py:242-243)
-        if (!__syncthreads_or((unfinished && c.row_valid) ? 1 : 0)) return false;
+        if (!__syncthreads_or(((unfinished && c.row_valid) || p.no_exit) ? 1 : 0)) return false;
     }
     if (t >= p.T) return false;
 
@@ -1871,10 +1881,14 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         __syncthreads();
     }
     pre = lpf;
+    PROF_AT(blockIdx.x, 1024, pm + 4);
     // ---- phase B: h_{t+1} complete in the group -> every workgroup reads all of it
     coop_arrive(ctr);
     ++phase;
+#if !(DECODE_ABLATE & 128)
     if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
+#endif
+    PROF_AT(blockIdx.x, 1024, pm + 5);
 #pragma unroll
     for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, HP_SLOT(hpar, i));
     return true;
@@ -2057,6 +2071,36 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
         }
     }
     if (n_launch) *n_launch = ne;
+    return hipGetLastError();
+}
+
+// seq_logprobs as FCModel._sample leaves them when a member's rows span several slabs: the reference
+// writes the greedy log-prob of EVERY row at every step until the whole batch has finished
+// (nets.py:240-243), so a decode with log-prob output runs every slab to step T (no_exit) and this pass
+// zeroes the steps after the batch's last finishing step (the reference's seq_logprobs start as zeros,
+// nets.py:191). One workgroup per (member, sign) rollout of B rows.
+__global__ __launch_bounds__(256) void nicnes_lp_batch_exit_kernel(const int32_t* seq, float* lp, int B, int T) {
+    __shared__ int last;
+    const size_t base = (size_t)blockIdx.x * B * T;
+    if (threadIdx.x == 0) last = 0;
+    __syncthreads();
+    int mine = 0;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+        int f = T - 1;                                   // a row that never emits the end token: all T steps
+        for (int t = 0; t < T; ++t)
+            if (seq[base + (size_t)b * T + t] == 0) { f = t; break; }
+        mine = max(mine, f);
+    }
+    atomicMax(&last, mine);
+    __syncthreads();
+    const int t_last = last;
+    for (int i = threadIdx.x; i < B * T; i += blockDim.x)
+        if (i % T > t_last) lp[base + i] = 0.f;
+}
+
+extern "C" hipError_t nicnes_launch_lp_batch_exit(const int32_t* seq, float* lp, int rollouts, int B, int T,
+                                                  hipStream_t stream) {
+    hipLaunchKernelGGL(nicnes_lp_batch_exit_kernel, dim3(rollouts), dim3(256), 0, stream, seq, lp, B, T);
     return hipGetLastError();
 }
 

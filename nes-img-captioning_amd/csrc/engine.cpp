@@ -732,6 +732,9 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     p.S = S;
     p.part = h->part;
     p.coop = coop_fits(h, G, nslabs, S, count) ? 1 : 0;
+    // log-probs of a batch spread over several slabs: every slab runs to T, then the steps after the
+    // batch's last finishing step are zeroed (nicnes_lp_batch_exit), as FCModel._sample leaves them
+    p.no_exit = (p.lp && nslabs > 1) ? 1 : 0;
     p.coop_ctr = h->coop_ctr;
     p.alive2 = h->alive + h->alive_stride;
     p.alive_stride = h->alive_stride;
@@ -783,6 +786,8 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     }
     h->n_dev = h->timing ? n_ev : 0;
     h->multi_stream = nstr > 1;
+    if (p.no_exit)
+        HIPC(h, nicnes_launch_lp_batch_exit(p.seq, p.lp, 2 * count, h->B, h->cfg.seq_length, s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     if (!h->stats_pending) {          // read the fallback counter back without a host wait
         HIPC(h, hipMemcpyAsync(h->stats_host, h->stats, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));

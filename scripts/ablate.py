@@ -102,6 +102,32 @@ def split_spans(k, seq, S=4):
         np.median(ph[0]), np.median(ph[1]), ' '.join('%.1f' % np.median(v) for v in ph[2:7]), np.median(ph[7])))
 
 
+def coop_spans(k, seq, S):
+    """DECODE_PROF=1 build, coop path (one launch, S workgroups per member slab): per step t = 1..15 the
+    median over workgroups of the logit loop, the phase-A wait (partials), the merge + token, the cell,
+    the phase-B wait (h'), and the read-back of h to the next step's start; then the logit loop per range q
+    (the slowest range sets the pace of its group)."""
+    raw = seq.reshape(-1, 1024).cpu().numpy().astype(np.int64) & 0xffffffff
+    ts = raw[:, :256]
+    nwg = ts.shape[0]
+    names = ('logit', 'waitA', 'token', 'cell', 'waitB', 'to_next')
+    ph = {n: [] for n in names}
+    per_q = [[] for _ in range(S)]
+    for t in range(1, 16):
+        b = 8 * (t + 1)
+        marks = [b, b + 1, b + 2, b + 3, b + 4, b + 5, b + 8]
+        for i, n in enumerate(names):
+            d = ((ts[:, marks[i + 1]] - ts[:, marks[i]]) % (1 << 32)) / 100.0
+            ph[n].append(np.median(d))
+        d = ((ts[:, b + 1] - ts[:, b]) % (1 << 32)) / 100.0
+        for q in range(S):
+            per_q[q].append(np.median(d[np.arange(nwg) % S == q]))
+    tot = ((ts[:, 8 * 17 + 1] - ts[:, 8 * 2]) % (1 << 32)) / 100.0
+    print(k, 'coop median per step t=1..15 (us):', ' '.join('%s %.2f' % (n, np.median(v)) for n, v in ph.items()))
+    print(k, 'coop logit loop by range q (us):', ' '.join('q%d %.2f' % (q, np.median(v)) for q, v in enumerate(per_q)))
+    print(k, 'coop steps 1..16 span per workgroup (us): median %.1f max %.1f' % (np.median(tot), tot.max()))
+
+
 def main():
     pop = int(os.environ.get('POP', '512'))
     rounds = int(os.environ.get('ROUNDS', '3'))
@@ -154,7 +180,10 @@ def main():
         for q, seq in enumerate(seqs):
             print('--- %s iteration %d of 3 (decode, CIDEr-D, ranks, noise sum, Adam), queued after a 50 ms idle'
                   % (k, q + 1))
-            if pop <= 64:
+            path = e.decode_path(128, pop)
+            if path == 'coop':
+                coop_spans(k, seq, e.decode_shape(128, pop)[2])
+            elif pop <= 64:
                 split_spans(k, seq)
             else:
                 launch_spans(k, seq)

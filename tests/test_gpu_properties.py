@@ -137,3 +137,39 @@ def test_forced_ties_follow_oracle(eng, copies):
             if fr[b, t]:
                 break
             assert seq[b, t] == oseq[b, t], (b, t)
+
+
+@pytest.mark.parametrize('S,G,coop', [(1, 4, 1), (4, 4, 0), (4, 4, 1), (4, 2, 0)],
+                         ids=['fused_2slabs', 'split_2slabs', 'coop_2slabs', 'split_G2_3slabs'])
+def test_logprobs_after_a_slab_exit_match_oracle(eng, S, G, coop):
+    """seq_logprobs of a batch that spans several slabs (B = 130): the reference writes the greedy
+    log-prob of every row, finished or not, until the WHOLE batch has finished (nets.py:240-243) and
+    leaves zeros after. With log-prob output the engine runs every slab to T and zeroes the steps after
+    the batch's last finishing step; staggered finishing (logit.bias[0] raised) makes slabs finish at
+    different steps. Every row and step against the oracle's whole-batch decode (1e-5, up to a row's
+    first lse-fragile step), tokens end to end."""
+    dims = O.Dims()
+    theta = O.make_theta(dims, 8, 4.0, 0.1)
+    theta[dims.offsets()['logit.bias'][0]] += np.float32(0.8)
+    fc = _fc(130, 55)
+    _load(eng, theta, fc)
+    eng.set_decode_split(S, G)
+    eng.set_decode_coop(coop)
+    try:
+        _, seq, lp = eng.evaluate(2, 0, 1, 0.0, return_seq=True, return_lp=True)
+        _, seq_nolp = eng.evaluate(2, 0, 1, 0.0, return_seq=True)
+    finally:
+        eng.set_decode_split(0, 0)
+        eng.set_decode_coop(1)
+    seq, lp = seq.cpu().numpy()[0, 0], lp.cpu().numpy()[0, 0]
+    assert np.array_equal(seq, seq_nolp.cpu().numpy()[0, 0])       # the run to T changes no token
+    oseq, olp, fr = O.decode(dims, theta, fc)
+    fin = np.array([np.argmax(r == 0) if (r == 0).any() else 16 for r in oseq])
+    slab = 32 * G
+    firsts = [fin[i:i + slab].max() for i in range(0, 130, slab)]
+    assert len(set(firsts)) > 1, firsts                             # the slabs do finish at different steps
+    assert fin.max() < 15                                           # and the batch before T
+    ok = ~np.cumsum(fr, 1).astype(bool)
+    assert np.array_equal(seq[ok], oseq[ok])
+    assert np.abs(lp[ok] - olp[ok]).max() <= 1e-5
+    assert (lp[:, fin.max() + 1:] == 0).all() and (olp[:, fin.max() + 1:] == 0).all()
