@@ -75,6 +75,9 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef LOGIT_MID_AT
 #define LOGIT_MID_AT 6     // ... before half-chunk LOGIT_MID_AT of 8 (measured: 5-7 equal, 2 and 8 -0.8 %)
 #endif
+#ifndef COOP_EARLY_H
+#define COOP_EARLY_H 1     // coop path: the first gate tile's h2h chain runs during the phase-A wait
+#endif
 #ifndef DECODE_PRIO
 #define DECODE_PRIO 0      // s_setprio 1 for one half of the workgroup's waves: 1 = waves 4-7, 2 = waves 0-3
 #endif
@@ -430,27 +433,27 @@ __device__ __forceinline__ f32x16 mfma_tile_o(f32x16 acc, const float* w, const 
 
 // cell stage: chain a = i2h tile (stage rows 0-31) over B = x, chain b = h2h tile (rows 32-63)
 // over B = h; k chunks [T0, T1) of 32 (init: start from the bias)
-template <int T0, int T1, bool H = true>
+template <int T0, int T1, bool H = true, bool X = true>
 __device__ __forceinline__ void mfma_xh_part(const float* w, const float* bias, const float (&Bx)[64],
                                              const float (&Bh)[64], int lane, f32x16& acc0, f32x16& acc1) {
     const int hh = lane >> 5;
     const float* row0 = w + (lane & 31) * LDS_ROW + hh * 16;
     const float* row1 = row0 + 32 * LDS_ROW;
     if (T0 == 0) {
-        acc0 = bias_init(bias, hh);
-        acc1 = bias_init(bias + 32, hh);
+        if (X) acc0 = bias_init(bias, hh);
+        acc1 = bias_init(bias + 32, hh);                 // H = false (h = 0): h2h(h) is its bias
     }
 #pragma unroll
     for (int T = T0; T < T1; ++T) {
         f32x4 a0[4], a1[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            a0[c] = *reinterpret_cast<const f32x4*>(row0 + T * 32 + 4 * c);
-            a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
+            if (X) a0[c] = *reinterpret_cast<const f32x4*>(row0 + T * 32 + 4 * c);
+            if (H) a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
         }
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) {
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bx[16 * T + jj], acc0, 0, 0, 0);
+            if (X) acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bx[16 * T + jj], acc0, 0, 0, 0);
             if (H) acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bh[16 * T + jj], acc1, 0, 0, 0);
         }
     }
@@ -1742,6 +1745,9 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
     };
     int it = 0;                                   // token fed to the next cell (0 = BOS at t = 0)
     bool cell_pre = false;                        // s64 holds the cell's first gate tile
+    bool tile_lds = false;                        // the cell's first gate tile is in LDS buffer 0
+    bool h_done = false;                          // acc_h holds that tile's h2h chain (b_h2h + W_h2h . h_t)
+    f32x16 acc_h;
     if (nl) {
         RowState st;
         row_state_init(st);
@@ -1765,6 +1771,18 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         }
         coop_arrive(ctr);
         ++phase;
+#if COOP_EARLY_H
+        // the h2h half of the first gate tile needs h_t only, not this step's token: it runs while the
+        // group's partial states are still arriving (i2h(x) + h2h(h) is summed in the same order after)
+        if (cell_pre) {
+            stage64_store(lds, 64, c.wave * 64 + lane_fresh(), s64);
+            __syncthreads();
+            f32x16 unused;
+            mfma_xh_part<0, 4, true, false>(lds + c.sgn * (64 * LDS_ROW), lds + 2 * 64 * LDS_ROW + 64 * c.sgn, hB, hB,
+                                            lane_fresh(), unused, acc_h);
+            tile_lds = h_done = true;
+        }
+#endif
 #if !(DECODE_ABLATE & 128)
         if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
 #endif
@@ -1783,7 +1801,7 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
             merge_exact(p, lds, c.wg, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.wave, c.lane, 1, S, hB, true,
                         PAIRS, m, lse, tok);
             if (q == 0 && c.tid == 0) atomicAdd(p.stats + 0, 1);
-            cell_pre = false;
+            cell_pre = tile_lds = false;           // (acc_h stays valid: registers)
         }
         if (tok >= p.V1) tok = 0;               // every logit NaN: end the caption (fused kernel rule)
         const bool unfinished = unf_prev != 0.f && tok > 0;
@@ -1823,9 +1841,11 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
 #pragma unroll
     for (int i = 0; i < 64; ++i) pin(xB[i]);
     const int hpar = (t + 1) & 1;
-    if (!cell_pre) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
-    stage64_store(lds, 64, c.wave * 64 + lane_fresh(), s64);
-    __syncthreads();
+    if (!tile_lds) {
+        if (!cell_pre) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
+        stage64_store(lds, 64, c.wave * 64 + lane_fresh(), s64);
+        __syncthreads();
+    }
     f32x16 hold;
     auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) __attribute__((always_inline)) {
         const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
@@ -1874,7 +1894,10 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         f32x16 a0, a1;
         if (t < 0)      // h = 0 before the first cell: h2h(h) is its bias (fma(w, 0, acc) == acc)
             mfma_xh_part<0, 4, false>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
-        else
+        else if (COOP_EARLY_H && h_done && m == m0) {          // the h2h chain ran during the phase-A wait
+            mfma_xh_part<0, 4, false>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
+            a1 = acc_h;
+        } else
             mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
         fold(m, a0 + a1, cpre);                                  // i2h(x) + h2h(h), nets.py:109-111
         if (m + 1 < m1) stage64_store(lds + ((m - m0 + 1) & 1) * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
