@@ -75,9 +75,6 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef LOGIT_MID_AT
 #define LOGIT_MID_AT 6     // ... before half-chunk LOGIT_MID_AT of 8 (measured: 5-7 equal, 2 and 8 -0.8 %)
 #endif
-#ifndef COOP_EARLY_H
-#define COOP_EARLY_H 1     // coop path: the first gate tile's h2h chain runs during the phase-A wait
-#endif
 #ifndef DECODE_PRIO
 #define DECODE_PRIO 0      // s_setprio 1 for one half of the workgroup's waves: 1 = waves 4-7, 2 = waves 0-3
 #endif
@@ -1745,9 +1742,6 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
     };
     int it = 0;                                   // token fed to the next cell (0 = BOS at t = 0)
     bool cell_pre = false;                        // s64 holds the cell's first gate tile
-    bool tile_lds = false;                        // the cell's first gate tile is in LDS buffer 0
-    bool h_done = false;                          // acc_h holds that tile's h2h chain (b_h2h + W_h2h . h_t)
-    f32x16 acc_h;
     if (nl) {
         RowState st;
         row_state_init(st);
@@ -1771,18 +1765,6 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         }
         coop_arrive(ctr);
         ++phase;
-#if COOP_EARLY_H
-        // the h2h half of the first gate tile needs h_t only, not this step's token: it runs while the
-        // group's partial states are still arriving (i2h(x) + h2h(h) is summed in the same order after)
-        if (cell_pre) {
-            stage64_store(lds, 64, c.wave * 64 + lane_fresh(), s64);
-            __syncthreads();
-            f32x16 unused;
-            mfma_xh_part<0, 4, true, false>(lds + c.sgn * (64 * LDS_ROW), lds + 2 * 64 * LDS_ROW + 64 * c.sgn, hB, hB,
-                                            lane_fresh(), unused, acc_h);
-            tile_lds = h_done = true;
-        }
-#endif
 #if !(DECODE_ABLATE & 128)
         if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
 #endif
@@ -1801,7 +1783,7 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
             merge_exact(p, lds, c.wg, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.wave, c.lane, 1, S, hB, true,
                         PAIRS, m, lse, tok);
             if (q == 0 && c.tid == 0) atomicAdd(p.stats + 0, 1);
-            cell_pre = tile_lds = false;           // (acc_h stays valid: registers)
+            cell_pre = false;
         }
         if (tok >= p.V1) tok = 0;               // every logit NaN: end the caption (fused kernel rule)
         const bool unfinished = unf_prev != 0.f && tok > 0;
@@ -1841,11 +1823,9 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
 #pragma unroll
     for (int i = 0; i < 64; ++i) pin(xB[i]);
     const int hpar = (t + 1) & 1;
-    if (!tile_lds) {
-        if (!cell_pre) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
-        stage64_store(lds, 64, c.wave * 64 + lane_fresh(), s64);
-        __syncthreads();
-    }
+    if (!cell_pre) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
+    stage64_store(lds, 64, c.wave * 64 + lane_fresh(), s64);
+    __syncthreads();
     f32x16 hold;
     auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) __attribute__((always_inline)) {
         const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
@@ -1894,10 +1874,7 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         f32x16 a0, a1;
         if (t < 0)      // h = 0 before the first cell: h2h(h) is its bias (fma(w, 0, acc) == acc)
             mfma_xh_part<0, 4, false>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
-        else if (COOP_EARLY_H && h_done && m == m0) {          // the h2h chain ran during the phase-A wait
-            mfma_xh_part<0, 4, false>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
-            a1 = acc_h;
-        } else
+        else
             mfma_xh_part<0, 4>(buf + c.sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * c.sgn, xB, hB, lane_fresh(), a0, a1);
         fold(m, a0 + a1, cpre);                                  // i2h(x) + h2h(h), nets.py:109-111
         if (m + 1 < m1) stage64_store(lds + ((m - m0 + 1) & 1) * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);

@@ -102,14 +102,14 @@ def split_spans(k, seq, S=4):
         np.median(ph[0]), np.median(ph[1]), ' '.join('%.1f' % np.median(v) for v in ph[2:7]), np.median(ph[7])))
 
 
-def coop_spans(k, seq, S):
+def coop_spans(k, seq, S, pop):
     """DECODE_PROF=1 build, coop path (one launch, S workgroups per member slab): per step t = 1..15 the
     median over workgroups of the logit loop, the phase-A wait (partials), the merge + token, the cell,
     the phase-B wait (h'), and the read-back of h to the next step's start; then the logit loop per range q
     (the slowest range sets the pace of its group)."""
     raw = seq.reshape(-1, 1024).cpu().numpy().astype(np.int64) & 0xffffffff
-    ts = raw[:, :256]
-    nwg = ts.shape[0]
+    nwg = S * pop                                  # the launch's workgroups (one 128-row slab per member)
+    ts = raw[:nwg, :256]
     names = ('logit', 'waitA', 'token', 'cell', 'waitB', 'to_next')
     ph = {n: [] for n in names}
     per_q = [[] for _ in range(S)]
@@ -182,7 +182,7 @@ def main():
                   % (k, q + 1))
             path = e.decode_path(128, pop)
             if path == 'coop':
-                coop_spans(k, seq, e.decode_shape(128, pop)[2])
+                coop_spans(k, seq, e.decode_shape(128, pop)[2], pop)
             elif pop <= 64:
                 split_spans(k, seq)
             else:
