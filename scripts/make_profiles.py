@@ -1,9 +1,11 @@
-"""Turn one profile_r02.sh run (gpurun_out/<TAG>/) into the committed profile files (dev tool):
+"""Turn one profile_r03.sh run (gpurun_out/<TAG>/) into the committed profile files (dev tool):
   profiles/<round>_kernel_stats_p<P>.csv       rocprofv3 --kernel-trace --stats summary of the bench
   profiles/<round>_decode_launches_p<P>.json   full-population launch averages (scripts/trace_summary.py)
-  profiles/<round>_pmc_<kernel>_p<P>_b128.json per-launch PMC counters + derived figures (pmc_summary.py)
+  profiles/<round>_pmc_<key>_p<P>_b128.json    per-launch PMC counters + derived figures (pmc_summary.py),
+                                               stamped with the decode sources' hash (bench.py reads it)
   profiles/<round>_bench_profiled_p<P>.json    the bench line printed under the profiler
-usage: python scripts/make_profiles.py TAG [ROUND]
+P = members per GPU: 512 -> the fused steps kernel, 128 / 64 -> the coop kernel (S = 2 / 4).
+usage: python scripts/make_profiles.py TAG [ROUND] [P ...]
 """
 import json
 import os
@@ -16,22 +18,26 @@ sys.path.insert(0, REPO)
 import bench  # noqa: E402
 
 tag = sys.argv[1]
-rnd = sys.argv[2] if len(sys.argv) > 2 else 'r02'
+rnd = sys.argv[2] if len(sys.argv) > 2 else 'r03'
+pops = [int(x) for x in sys.argv[3:]] or [512, 128, 64]
 src = os.path.join(REPO, 'gpurun_out', tag)
 out = os.path.join(REPO, 'profiles')
 B = 128
-for P, key, kernel in ((512, 'steps', 'nicnes_decode_steps_kernel'), (64, 'logit', 'nicnes_decode_logit_kernel')):
+KERNELS = {512: ('steps', 'nicnes_decode_steps_kernel'), 256: ('steps', 'nicnes_decode_steps_kernel'),
+           128: ('coop2', 'nicnes_decode_coop_kernel<true, 2>'), 64: ('coop4', 'nicnes_decode_coop_kernel<true, 4>')}
+for P in pops:
+    key, kernel = KERNELS[P]
     st = os.path.join(src, 'stats%d' % P)
     shutil.copy(os.path.join(st, 'run_kernel_stats.csv'), os.path.join(out, '%s_kernel_stats_p%d.csv' % (rnd, P)))
     launches = os.path.join(out, '%s_decode_launches_p%d.json' % (rnd, P))
     subprocess.check_call([sys.executable, os.path.join(REPO, 'scripts', 'trace_summary.py'), '--trace', st,
                            '--out', launches, '--command', 'python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline '
-                           '--pop-per-gpu %d' % P], stdout=subprocess.DEVNULL)
+                           '--population %d' % P], stdout=subprocess.DEVNULL)
     with open(launches) as f:
         lj = json.load(f)
-    rec = [v for k, v in lj['kernels'].items() if kernel in k][0]
+    rec = [v for k, v in lj['kernels'].items() if kernel.split('<')[0] in k][0]
     dur_ms = rec['mean_ms_full_grid']
-    if key in ('step', 'steps'):
+    if key in ('step', 'steps', 'coop2', 'coop4'):
         n_launch = 18 if key == 'step' else 1           # one launch per step, or every step in one launch
         flop = bench.step_flops_per_member(B) * P / n_launch
         alg = bench.step_noise_bytes_per_member(B) * P / n_launch
@@ -42,9 +48,10 @@ for P, key, kernel in ((512, 'steps', 'nicnes_decode_steps_kernel'), (64, 'logit
     for i in range(4):
         passes += ['--pass', os.path.join(src, 'pmc%d_%d' % (P, i))]
     pmc = os.path.join(out, '%s_pmc_%s_p%d_b%d.json' % (rnd, key, P, B))
-    subprocess.check_call([sys.executable, os.path.join(REPO, 'scripts', 'pmc_summary.py'), '--kernel', kernel] + passes +
+    subprocess.check_call([sys.executable, os.path.join(REPO, 'scripts', 'pmc_summary.py'), '--kernel',
+                           kernel.split('<')[0]] + passes +
                           ['--duration-ms', '%.6f' % dur_ms, '--algorithmic-bytes', str(alg), '--algorithmic-flop',
-                           str(flop), '--note', 'bench.py --pop-per-gpu %d (B=128), rocprofv3 --pmc passes of %s; '
+                           str(flop), '--note', 'bench.py --population %d (B=128), rocprofv3 --pmc passes of %s; '
                            'duration = full-grid launch average of the kernel-trace run' % (P, tag), '--out', pmc])
     with open(os.path.join(src, 'stats%d.log' % P)) as f:
         lines = [l for l in f.read().splitlines() if l.startswith('{"metric"')]
