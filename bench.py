@@ -190,6 +190,10 @@ def main():
                     "--preset configs4)")
     ap.add_argument('--fitness', default='greedy', help="policy_options.fitness: greedy (mscoco_nes.json) or "
                     "greedy_logprob / greedy_expprob / greedy_linprob / greedy_avgprob")
+    ap.add_argument('--mutation', default='', choices=['', 'SM-G-SUM', 'SM-PROPORTIONAL'],
+                    help="model_options.safe_mutations (mscoco_nes.json: '', underflow 0.1): the per-task mutation "
+                    "vector is recomputed from each iteration's theta on the host (nicnes.mutations) inside the "
+                    "timed step, as reference workers do per task")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--decode-split', type=int, default=0, help='force S logit workgroups per member (0 = auto)')
     ap.add_argument('--decode-rows', type=int, default=0, help='force 4 (128-row) or 2 (64-row) slabs (0 = auto)')
@@ -235,14 +239,33 @@ def main():
             dist.init_process_group(backend)
     eng = nicnes.Engine(max_batch=B, max_members=P_local, noise_len=args.noise_len, noise_seed=0,
                         device=dev)
-    S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu, batches=args.batches,
-                            theta_gain=args.theta_gain, bias_std=args.bias_std)
+    wl = S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu, batches=args.batches,
+                                 theta_gain=args.theta_gain, bias_std=args.bias_std)
     eng.set_fitness_mode(args.fitness)
     eng.set_decode_split(args.decode_split, args.decode_rows)
     runner = PopulationRunner(eng, P, args.sigma, l2coeff=1e-7, stepsize=1e-3, rank=rank, world_size=world,
                               group=group)
+    mut_s = []
+    if args.mutation:
+        # SM-G-SUM: Sensitivity.calc_sensitivity of the task's theta on its batch (safe_mutations.py:34-117),
+        # per iteration; SM-PROPORTIONAL: |theta'| (nets.py:108-112)
+        from types import SimpleNamespace
+        from nicnes.mutations import Mutator
+        spec = SimpleNamespace(model_options=SimpleNamespace(safe_mutations=args.mutation, safe_mutation_underflow=0.1,
+                                                             safe_mutation_vector=''), batch_size=B)
+        mutator = Mutator(spec, eng)
+        fc_rows = wl['fc'][:B]
+
+        def prepare(it_):
+            t_ = time.perf_counter()
+            mutator.prepare(it_, eng.theta()[1], fc_rows)
+            mut_s.append(time.perf_counter() - t_)
+    else:
+        def prepare(it_):
+            pass
     it = 1
     for _ in range(args.warmup):
+        prepare(it)
         runner.step(it, sync=False, n_batches=args.batches)
         it += 1
     eng.set_timing(True)
@@ -251,7 +274,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    mut_s.clear()
     for _ in range(args.steps):
+        prepare(it)                                            # host sensitivity (waits for the last theta)
         runner.step(it, sync=False, n_batches=args.batches)   # enqueue only (a batch map is one small copy)
         it += 1
     torch.cuda.synchronize()
@@ -289,6 +314,8 @@ def main():
         # shape's every step in one launch (nicnes_decode_coop_kernel, S workgroups per member slab)
         if path == 'coop':
             kname = 'nicnes_decode_coop_kernel<%d>' % S_split
+        elif G == 2:                                 # 64-row slabs: nicnes_decode_steps2_kernel
+            kname = 'nicnes_decode_steps2_kernel'
         else:
             kname = 'nicnes_decode_steps_kernel' if ph['step_launches'] == 1 else 'nicnes_decode_step_kernel'
         n_step = ph['step_launches']
@@ -322,7 +349,8 @@ def main():
                                + (', theta gain %g bias std %g (not the reference init)' % (args.theta_gain, args.bias_std)
                                   if (args.theta_gain != 1.0 or args.bias_std) else '')
                                + (', %d batches per iteration (single_batch false: member i on batch i mod %d)'
-                                  % (args.batches, args.batches) if args.batches > 1 else ''),
+                                  % (args.batches, args.batches) if args.batches > 1 else '')
+                               + (', safe_mutations %s' % args.mutation if args.mutation else ''),
                    'population': P, 'members_per_gpu': P_local, 'batch_size': B, 'batches_per_iteration': args.batches,
                    'seq_length': 16,
                    'vocab_size': 9487,
@@ -357,6 +385,11 @@ def main():
         'cpu_baseline': cpu,
         'decodes_per_s': round(2 * value, 3),        # one decode = one sign's rollout of the batch
         'tie_fallbacks': eng.stats()['tie_fallbacks'],
+        'mutation': ({'mode': args.mutation, 'host_vector_s_per_iteration': round(float(np.mean(mut_s)), 4),
+                      'host_share_of_iteration': round(float(np.sum(mut_s)) / dt, 4),
+                      'note': 'the per-task mutation vector on the host CPU (torch autograd for SM-G-SUM: 95 '
+                              'backward passes of a 5-step decode, safe_mutations.py:93-117)'}
+                     if args.mutation else None),
         'update_ratio': ratio,
     }
     if rank == 0:

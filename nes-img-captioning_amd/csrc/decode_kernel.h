@@ -40,6 +40,7 @@ struct DecodeParams {
 #define DK_CELL 2        // split path: token merge of t + cell of t + 1
 #define DK_LOGIT 3       // split path: logits of t over one vocabulary range
 #define DK_COOP 5        // coop path: every step of the split shape in one launch
+#define DK_STEPS2 6      // fused path of 64-row slabs (G = 2, S = 1), every step in one launch
 
 // evs (nullable): up to DECODE_MAX_EVENTS events, recorded before the first launch and after every
 // launch; kinds[k] (k >= 1) is the kind of the launch that event k follows. Returns the launch count

@@ -57,6 +57,9 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef MFMA_FIRST_SIGN
 #define MFMA_FIRST_SIGN 0  // logit stages: the sign whose waves run the stage's MFMAs before the previous epilogue
 #endif
+#ifndef DECODE_FUSED2
+#define DECODE_FUSED2 1    // 64-row slabs with S = 1: every step in one launch (nicnes_decode_steps2_kernel)
+#endif
 #ifndef DECODE_PERSISTENT
 #define DECODE_PERSISTENT 1  // fused path: every step of a workgroup in one launch (0: one launch per step)
 #endif
@@ -1927,6 +1930,209 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_coop_kernel(DecodePara
         if (!coop_step<PAIRS, S>(p, c, q, lds, t, s64, pre, hB, ctr, phase)) break;
 }
 
+// ========== fused path for 64-row slabs (G = 2): every step of a workgroup in one launch =========
+// B <= 64 (mscoco_nes.json's own batch_size 64) with one workgroup per member slab (S = 1): wave w =
+// sign (w >> 2) x 32-row group ((w >> 1) & 1) x tile half (w & 1), as on the split path. Per step the
+// two tile halves of a row group scan opposite halves of each 64-row logit stage; their partial greedy
+// states go through memory (the workgroup's own part_ptr slots) to the half-0 waves, which merge them
+// exactly as the split cell kernel does (nh = 2), pick the token and fold the cell; in every gate tile
+// the half-1 waves run the h2h chain over h and hand it over in LDS (nicnes_decode_cell_kernel<2>).
+// h' crosses steps in the lane scratch of the row group (parity slots), read back by both halves.
+template <bool PAIRS>
+__device__ __forceinline__ bool step_body2(const DecodeParams& p, const SCtx<2>& c, float* lds, int t,
+                                           Stage64Regs& s64, bool& pre, float (&hB)[64]) {
+    PROF_AT(c.wg, 4096, 2 * (t + 1));
+    const uint32_t lo = 4u * c.lane;
+    const int nst = (p.V1 + 63) >> 6;
+    __builtin_assume(nst > 0);                     // (as in coop_step: no zero-trip logit loop)
+    const bool nl = t > 0;
+    const bool folder = c.hf == 0;                 // waves that own the rows' token and the cell fold
+    const uint64_t nidx = p.noise_idx[c.member];
+    const float unf_prev = (nl && folder) ? ld1(c.scr_r, lo, U_SLOT) : 0.f;
+    if (t < 0) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) hB[i] = 0.f;               // h = 0 before the first cell
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) pin(hB[i]);
+    const uint32_t ib = (uint32_t)p.off_i2h_b, hb = (uint32_t)p.off_h2h_b, bmin = min(ib, hb);
+    auto csrc = [&](int m) {                                     // gate tile m: i2h rows | h2h rows
+        const uint32_t r = gate_row(m);
+        StageSrc Sx;
+        Sx.w_r = c.theta_r; Sx.z_r = c.noise_r; Sx.b_r = c.theta_r; Sx.bz_r = c.noise_r;
+        Sx.so_a = 4u * ((uint32_t)p.off_i2h_w + 128u * r);
+        Sx.so_b = 4u * ((uint32_t)p.off_h2h_w + 128u * r);
+        Sx.bso = 4u * (bmin + r);
+        Sx.bda = 4u * (ib - bmin); Sx.bdb = 4u * (hb - bmin);
+        Sx.valid = 64;
+        return Sx;
+    };
+    int it = 0;                                   // token fed to the next cell (0 = BOS at t = 0)
+    bool cell_pre = false;                        // s64 holds the cell's first gate tile
+    if (nl) {
+        RowState st;
+        row_state_init(st);
+        auto tail = [&]() __attribute__((always_inline)) {
+            if (CROSS_PREFETCH && t < p.T) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
+        };
+        logit_stages<2, PAIRS>(lds, p, nidx, c.wave, c.sgn, c.hf, hB, 0, nst, st, s64, pre && LOGIT_MIDSTORE, tail);
+        cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && t < p.T;
+        {   // this tile half's partial greedy state (read back by the half-0 wave of the row group)
+            float* pb = part_ptr(p, c.wg, 0, c.wave) + lane_fresh();
+            pb[0] = st.m;
+            pb[64] = st.s;
+            pb[128] = st.r0v;
+            pb[192] = __builtin_bit_cast(float, st.r0i);
+            pb[256] = st.r1v;
+            pb[320] = __builtin_bit_cast(float, st.r1i);
+            pb[384] = st.ev;
+        }
+        __syncthreads();
+        float m = 0.f, lse = 0.f;
+        int tok = 0x7fffffff;
+        bool ovf = false;
+        if (folder) {
+            Part8 pr;
+            load_part8(p, c.wg, c.wave, lane_fresh(), 2, 2, 0, pr);
+            merge_partials(p, c.wg, c.wave, lane_fresh(), 2, 2, pr, PAIRS, m, lse, tok, ovf);
+        }
+        if (__syncthreads_or((p.force_exact || ovf) ? 1 : 0)) {
+            merge_exact(p, lds, c.wg, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.wave, c.lane, 2, 2, hB, folder,
+                        PAIRS, m, lse, tok);
+            if (c.tid == 0) atomicAdd(p.stats + 0, 1);
+            cell_pre = false;                   // the exact sweep staged through LDS with its own registers
+        }
+        if (tok >= p.V1) tok = 0;               // every logit NaN: end the caption (fused kernel rule)
+        const bool unfinished = unf_prev != 0.f && tok > 0;
+        it = unfinished ? tok : 0;
+        if (folder) {
+            st1(c.scr_r, lo, U_SLOT, unfinished ? 1.f : 0.f);
+#if !DECODE_PROF
+            if (c.hh == 0 && c.row_valid) {
+                const size_t o = (((size_t)c.member * 2 + c.sgn) * p.B + c.b) * p.T + (t - 1);
+                p.seq[o] = it;
+                if (p.lp) p.lp[o] = -lse;       // seq_logprobs[:, t-1] (nets.py:208,241)
+            }
+#endif
+        }
+        const int any = __syncthreads_or(((folder && unfinished && c.row_valid) || p.no_exit) ? 1 : 0);
+        if (!any) return false;                 // the reference stops here (nets.py:242-243)
+    }
+    if (t >= p.T) return false;
+
+    // ---- LSTM cell of step t+1 (nets.py:98-134): half 0 i2h over x, half 1 h2h over h -------------
+    float xB[64];
+    if (!folder) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) xB[i] = 0.f;
+    } else if (t < 0) {                                          // x = img_embed(fc) (nets.py:194-195)
+#pragma unroll
+        for (int i = 0; i < 64; ++i) xB[i] = ld1(c.scr_r, lo, X_SLOT(i));
+    } else {                                                     // x = embed(it) (nets.py:196-199)
+        const uint32_t eo = 4u * ((uint32_t)p.off_emb_w + (uint32_t)it * 128u + 4u * c.hh);
+#pragma unroll
+        for (int T = 0; T < 4; ++T)
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const f32x4 w = ld4(c.theta_r, eo + 4u * (32 * T + 8 * a));
+                const f32x4 z = ld4(c.noise_r, eo + 4u * (32 * T + 8 * a));
+                const f32x4 x = c.sgn ? (w - z) : (w + z);         // the table is sigma-scaled
+#pragma unroll
+                for (int e = 0; e < 4; ++e) xB[16 * T + 4 * a + e] = x[e];
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) pin(xB[i]);
+    const int hpar = (t + 1) & 1;
+    if (!cell_pre) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
+    stage64_store(lds, 64, c.wave * 64 + lane_fresh(), s64);
+    __syncthreads();
+    f32x16 hold;
+    auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) __attribute__((always_inline)) {
+        const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
+        const int U = m / 5, j5 = m % 5;
+        if (j5 == 0) {                                           // g1
+            hold = s_;
+        } else if (j5 == 1) {                                    // g = max(g1, g2)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hold[r] = hold[r] > s_[r] ? hold[r] : s_[r];
+        } else if (j5 == 2) {                                    // ig * g
+#pragma unroll
+            for (int r = 0; r < 16; ++r) hold[r] = CELL_SIG(s_[r]) * hold[r];
+        } else if (j5 == 3) {                                    // c' = f * c + ig * g
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float fcv = CELL_SIG(s_[r]) * cpre[r];
+                const float cn = fcv + hold[r];
+                st1(c.scr_r, lo_, C_SLOT(16 * U + r), cn);
+                hold[r] = cn;
+            }
+        } else {                                                 // h' = o * tanh(c')
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                st1(c.scr_r, lo_, HP_SLOT(hpar, 16 * U + r), CELL_SIG(s_[r]) * CELL_TANH(hold[r]));
+        }
+    };
+    auto load_c = [&](int m) __attribute__((always_inline)) {   // c of the f tile's unit block
+        f32x16 cp;
+        const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cp[r] = (m % 5 == 3 && t >= 0) ? ld1(c.scr_r, lo_, C_SLOT(16 * (m / 5) + r)) : 0.f;
+        return cp;
+    };
+    float* xch = lds + 2 * STAGE64_FLOATS + (c.sgn * 2 + c.grp) * 1024;   // h2h half -> i2h half
+    const bool lpf = LOGIT_MIDSTORE && CROSS_PREFETCH && t >= 0;          // the next step's first logit tile
+#pragma unroll 1
+    for (int m = 0; m < 20; ++m) {
+        const f32x16 cpre = load_c(m);
+        __builtin_amdgcn_sched_barrier(0);
+        if (m + 1 < 20) {
+            stage64_load(csrc(m + 1), c.wave * 64 + lane_fresh(), s64);
+        } else if (lpf) {
+            const LaneOffs lo_ = lane_offs(c.wave, 128u);
+            stage64_load_o(logit_src(p, nidx, 0), lo_, c.wave < 2, s64);
+        }
+        const float* buf = lds + (m & 1) * STAGE64_FLOATS;
+        const float* w1 = buf + c.sgn * (64 * LDS_ROW) + 32 * c.hf * LDS_ROW;
+        const float* b1 = buf + 2 * 64 * LDS_ROW + 64 * c.sgn + 32 * c.hf;
+        f32x16 a = bias_init(b1, lane_fresh() >> 5);
+        if (folder) a = mfma_tile(a, w1, xB, lane_fresh());
+        else if (t >= 0) a = mfma_tile(a, w1, hB, lane_fresh());   // h = 0 before the first cell: the bias
+        if (!folder) {
+            const int l = lane_fresh();
+#pragma unroll
+            for (int r = 0; r < 16; ++r) xch[r * 64 + l] = a[r];
+        }
+        __syncthreads();
+        if (folder) {
+            const int l = lane_fresh();
+            f32x16 a1;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a1[r] = xch[r * 64 + l];
+            fold(m, a + a1, cpre);                               // i2h(x) + h2h(h), nets.py:109-111
+        }
+        if (m + 1 < 20) stage64_store(lds + ((m + 1) & 1) * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
+        __syncthreads();
+    }
+    pre = lpf;
+    // h_{t+1}: the half-0 waves' h' stores of the row group, read back by both halves
+#pragma unroll
+    for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, HP_SLOT(hpar, i));
+    PROF_AT(c.wg, 4096, 2 * (t + 1) + 1);
+    return true;
+}
+
+template <bool PAIRS>
+__global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps2_kernel(DecodeParams p) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const SCtx<2> c = make_sctx<2>(p);            // grid (1, members, slabs)
+    Stage64Regs s64;
+    bool pre = false;
+    float hB[64];
+    for (int t = -1; t <= p.T; ++t)
+        if (!step_body2<PAIRS>(p, c, lds, t, s64, pre, hB)) break;
+}
+
 namespace {
 const size_t LDS64 = (size_t)(2 * STAGE64_FLOATS) * sizeof(float);
 const size_t LDS32 = (size_t)(2 * STAGE_FLOATS) * sizeof(float);
@@ -1951,6 +2157,8 @@ extern "C" hipError_t nicnes_decode_init() {
         {(const void*)nicnes_decode_coop_kernel<true, 4>, LDS64},
         {(const void*)nicnes_decode_coop_kernel<false, 4>, LDS64},
         {(const void*)nicnes_decode_cell_kernel<2>, LDS_CELL2},
+        {(const void*)nicnes_decode_steps2_kernel<true>, LDS_CELL2},
+        {(const void*)nicnes_decode_steps2_kernel<false>, LDS_CELL2},
         {(const void*)nicnes_decode_img_kernel<4>, LDS32},
         {(const void*)nicnes_decode_img_kernel<2>, LDS32},
     };
@@ -2054,6 +2262,15 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
                 hipLaunchKernelGGL(nicnes_decode_cell_kernel<4>, gc, block, LDS64, stream, *p, t);
                 mark(DK_CELL);
             }
+        } else if (p->S == 1 && DECODE_FUSED2 && !DECODE_PROF) {
+            // 64-row slabs, one workgroup per member slab: every step in one launch
+            hipLaunchKernelGGL(nicnes_decode_img_kernel<2>, gc, block, LDS32, stream, *p);
+            mark(DK_IMG);
+            if (pairs)
+                hipLaunchKernelGGL(nicnes_decode_steps2_kernel<true>, gc, block, LDS_CELL2, stream, *p);
+            else
+                hipLaunchKernelGGL(nicnes_decode_steps2_kernel<false>, gc, block, LDS_CELL2, stream, *p);
+            mark(DK_STEPS2);
         } else {
             hipLaunchKernelGGL(nicnes_decode_img_kernel<2>, gc, block, LDS32, stream, *p);
             mark(DK_IMG);

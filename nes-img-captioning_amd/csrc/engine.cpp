@@ -758,7 +758,7 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
     int n_ev = 0;
     // the coop launch needs all its workgroups resident: never split over streams
-    const int nstr = p.coop ? 1 : std::min(count, h->dec_streams ? h->dec_streams : ((G == 4 && S == 1) ? 1 : 2));
+    const int nstr = p.coop ? 1 : std::min(count, h->dec_streams ? h->dec_streams : (S == 1 ? 1 : 2));
     if (nstr > 1) {
         // members split evenly over the caller's stream and nstr - 1 engine streams; the parts share
         // nothing but the fallback counter (an atomic). No per-launch events: the launches overlap
@@ -970,6 +970,7 @@ int nicnes_decode_phase_times(nicnes_handle* h, float* out8_host) {
                 break;
             case DK_STEPS: o[2] += ms; o[3] += 1; break;      // every step in one launch
             case DK_COOP: o[2] += ms; o[3] += 1; break;       // the split shape, every step in one launch
+            case DK_STEPS2: o[2] += ms; o[3] += 1; break;     // 64-row slabs, every step in one launch
             case DK_LOGIT: o[4] += ms; o[5] += 1; break;
             default:
                 o[6] += ms; o[7] += 1;
@@ -997,7 +998,7 @@ int nicnes_decode_path(nicnes_handle* h, int32_t B, int32_t count, int32_t* out_
     if (!h || !out_host || B < 1 || count < 1) return NICNES_ERR_INVALID;
     int G = 0, nslabs = 0, S = 0;
     decode_shape(h, B, count, &G, &nslabs, &S);
-    *out_host = (G == 4 && S == 1) ? 0 : coop_fits(h, G, nslabs, S, count) ? 2 : 1;
+    *out_host = S == 1 ? 0 : coop_fits(h, G, nslabs, S, count) ? 2 : 1;
     return NICNES_OK;
 }
 

@@ -72,7 +72,8 @@ def test_decode_path_rule(eng):
     assert eng.decode_path(128, 64) == 'coop' and eng.decode_shape(128, 64) == (4, 1, 4)
     assert eng.decode_path(128, 128) == 'coop' and eng.decode_shape(128, 128) == (4, 1, 2)
     assert eng.decode_path(128, 256) == 'fused' and eng.decode_path(128, 512) == 'fused'
-    assert eng.decode_path(64, 64) == 'split'                  # 64-row slabs stay on the two-launch path
+    assert eng.decode_path(64, 64) == 'split'                  # 64-row slabs stay on the two-launch path ...
+    assert eng.decode_path(64, 512) == 'fused' and eng.decode_shape(64, 512) == (2, 1, 1)   # ... unless S = 1
     assert eng.decode_path(130, 64) == 'split'                 # B = 130 pads least with 64-row slabs
     eng.set_decode_split(0, 4)                                # forced 128-row slabs: two of them
     try:

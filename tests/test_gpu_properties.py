@@ -139,8 +139,8 @@ def test_forced_ties_follow_oracle(eng, copies):
             assert seq[b, t] == oseq[b, t], (b, t)
 
 
-@pytest.mark.parametrize('S,G,coop', [(1, 4, 1), (4, 4, 0), (4, 4, 1), (4, 2, 0)],
-                         ids=['fused_2slabs', 'split_2slabs', 'coop_2slabs', 'split_G2_3slabs'])
+@pytest.mark.parametrize('S,G,coop', [(1, 4, 1), (4, 4, 0), (4, 4, 1), (4, 2, 0), (1, 2, 0)],
+                         ids=['fused_2slabs', 'split_2slabs', 'coop_2slabs', 'split_G2_3slabs', 'fused_G2_3slabs'])
 def test_logprobs_after_a_slab_exit_match_oracle(eng, S, G, coop):
     """seq_logprobs of a batch that spans several slabs (B = 130): the reference writes the greedy
     log-prob of every row, finished or not, until the WHOLE batch has finished (nets.py:240-243) and

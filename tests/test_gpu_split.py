@@ -158,7 +158,7 @@ def test_split_shard_invariance(eng):
 
 
 @pytest.mark.parametrize('bias0', [40.0, 1.0, 0.8])
-@pytest.mark.parametrize('G,S', [(4, 4), (2, 4), (4, 1)], ids=['G4S4', 'G2S4', 'fused'])
+@pytest.mark.parametrize('G,S', [(4, 4), (2, 4), (4, 1), (2, 1)], ids=['G4S4', 'G2S4', 'fused', 'fused_G2'])
 def test_early_exit_matches_oracle(eng, G, S, bias0):
     """logit.bias[0] raised so rows emit the end token at step 1 (all finish at once), or at
     staggered steps: the split alive chain must stop exactly where the reference stops
@@ -242,7 +242,7 @@ def test_split_forced_ties_follow_oracle(eng, G, S):
         assert _mismatch(seq.cpu().numpy()[0, 0], oseq, fr) == [], (k_tie, dsts)
 
 
-@pytest.mark.parametrize('S,G', [(4, 4), (1, 4), (4, 2)], ids=['split_G4S4', 'fused', 'split_G2S4'])
+@pytest.mark.parametrize('S,G', [(4, 4), (1, 4), (4, 2), (1, 2)], ids=['split_G4S4', 'fused', 'split_G2S4', 'fused_G2'])
 def test_decode_streams_do_not_change_results(eng, S, G):
     """members split over 1..4 streams (nicnes_set_decode_streams; 7 members split unevenly, ragged
     100-row slabs): fitness, tokens and log-probs bit-identical to the one-stream decode"""
