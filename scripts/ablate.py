@@ -130,6 +130,7 @@ def coop_spans(k, seq, S, pop):
 
 def main():
     pop = int(os.environ.get('POP', '512'))
+    B = int(os.environ.get('BATCH', '128'))
     rounds = int(os.environ.get('ROUNDS', '3'))
     libs = sorted(glob.glob(os.path.join(REPO, 'nes-img-captioning_amd', 'build', 'ablate', 'libnicnes_*.so')))
     noise = torch.from_numpy(S.noise_table(1 << 27)).cuda()
@@ -141,9 +142,9 @@ def main():
     wl = None
     for path in libs:
         name = os.path.basename(path)[len('libnicnes_'):-3]
-        e = nicnes.Engine(max_batch=128, max_members=pop, noise_len=1 << 27, lib_path=path)
+        e = nicnes.Engine(max_batch=B, max_members=pop, noise_len=1 << 27, lib_path=path)
         if wl is None:
-            wl = S.setup_engine_workload(e, B=128, noise=noise)
+            wl = S.setup_engine_workload(e, B=B, noise=noise)
             keys, vals = nicnes.df_table_arrays(wl['df'])
         else:                                   # timing-only builds decode garbage: reuse base's refs
             e.set_noise_table(noise)
@@ -180,9 +181,9 @@ def main():
         for q, seq in enumerate(seqs):
             print('--- %s iteration %d of 3 (decode, CIDEr-D, ranks, noise sum, Adam), queued after a 50 ms idle'
                   % (k, q + 1))
-            path = e.decode_path(128, pop)
+            path = e.decode_path(B, pop)
             if path == 'coop':
-                coop_spans(k, seq, e.decode_shape(128, pop)[2], pop)
+                coop_spans(k, seq, e.decode_shape(B, pop)[2], pop)
             elif pop <= 64:
                 split_spans(k, seq)
             else:
