@@ -238,6 +238,15 @@ int nicnes_set_decode_streams(nicnes_handle* h, int32_t n);
  * greedy states and h' to each other (mode 1, the default; env NICNES_DECODE_COOP=0/1 sets the initial
  * value), instead of two launches per step (mode 0). Tokens do not depend on it. */
 int nicnes_set_decode_coop(nicnes_handle* h, int32_t mode);
+
+/* SM-G-SUM sensitivity of the current theta on the first `rows` images of the batch held (batch 0):
+ * replaces Sensitivity.calc_sensitivity / _calc_sum_sensitivity (src/algorithm/safe_mutations.py:34-117)
+ * on CaptionModel.forward_for_sensitivity (src/captioning/nets.py:22-70; length 5, groups of 100).
+ * out (device, D floats) = sqrt(sum_k J[k, :]^2) / rows, clamped to >= underflow and divided by it
+ * (safe_mutations.py:63-65; underflow <= 0: the raw vector). The greedy tokens come from the engine's
+ * bit-exact decode; the K = V1 / 100 + 1 backward passes run batched on the GPU, so the vector agrees
+ * with the reference's to fp32 rounding (a stated tolerance), not bit for bit. Asynchronous on stream. */
+int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, float* out_dev, void* stream);
 /* the decode path an evaluate of `count` members of a B-image batch would take: 0 fused (one launch,
  * one workgroup per member slab), 1 split (two launches per step), 2 coop (the split shape in one launch) */
 int nicnes_decode_path(nicnes_handle* h, int32_t B, int32_t count, int32_t* out_host);

@@ -22,6 +22,7 @@ struct DecodeParams {
     uint32_t* coop_ctr;          // coop path: [members * slabs] x 32 hand-off counters (zeroed per launch)
     int32_t coop;                // 1: the split shape (G = 4, S = 2 or 4) in one persistent launch
     int32_t no_exit;             // 1: no per-slab early exit (log-probs of a multi-slab batch, see below)
+    int32_t no_mask;             // 1 (fused path): feed every argmax back unmasked (forward_for_sensitivity)
     int32_t force_exact;         // test hook (NICNES_FORCE_EXACT=1): every step takes the exact tie pass
     float lse_margin;            // widening of the bounded-lse interval: 2e-3 (test hook NICNES_LSE_MARGIN)
     int32_t bounded_lse;         // 1: greedy-only decode with the pair-bounded lse (needs lp == NULL)

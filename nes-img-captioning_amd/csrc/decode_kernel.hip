@@ -1172,9 +1172,9 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         // no candidate only when every logit is NaN (torch.max would return a NaN's index):
         // end the caption instead of emitting an out-of-vocabulary id
         if (tok >= p.V1) tok = 0;
-        // finished mask (nets.py:236-243)
+        // finished mask (nets.py:236-243); forward_for_sensitivity feeds every argmax back (nets.py:62-63)
         const bool unfinished = unf_prev != 0.f && tok > 0;
-        it = unfinished ? tok : 0;
+        it = (unfinished || p.no_mask) ? tok : 0;
         st1(c.scr_r, lo, U_SLOT, unfinished ? 1.f : 0.f);
 #if !DECODE_PROF
         if (c.hh == 0 && c.row_valid) {

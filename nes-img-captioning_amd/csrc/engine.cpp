@@ -19,6 +19,7 @@
 #include "cider_kernel.h"
 #include "decode_kernel.h"
 #include "update_kernels.h"
+#include "sensitivity.h"
 
 #define MB_RING 4   // pinned staging slots of the member -> batch map (nicnes_evaluate_batches)
 
@@ -106,6 +107,10 @@ struct nicnes_handle {
     int dec_streams = 0;
     int coop_mode = 1;                // nicnes_set_decode_coop: 0 never, 1 the split shape in one launch when it fits
     uint32_t* coop_ctr = nullptr;     // [max_members * slabs * COOP_CTR_STRIDE] coop hand-off counters
+    SensWork* sens = nullptr;         // SM-G-SUM sensitivity work buffers (nicnes_sum_sensitivity)
+    float* zero_noise = nullptr;      // [D] zeros + one zero index: the sigma = 0 decode of the sensitivity
+    uint64_t* zero_idx = nullptr;
+    int32_t* sens_tok = nullptr;      // [2 * max_batch * 4] its greedy tokens
     hipStream_t sx[3] = {nullptr, nullptr, nullptr};
     hipEvent_t ev_fork = nullptr;
     hipEvent_t ev_join[3] = {nullptr, nullptr, nullptr};
@@ -394,7 +399,9 @@ int nicnes_destroy(nicnes_handle* h) {
     void* bufs[] = {h->theta64, h->theta32, h->m, h->v, h->ref_keys, h->ref_vec, h->ref_count, h->ref_len2,
                     h->ref_norm, h->nidx, h->seq, h->lp, h->row_scores, h->dscratch, h->stats, h->partials, h->norms,
                     h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive, h->part,
-                    h->rank_key, h->rank_idx, h->mbatch, h->mut_vec, h->dbuf, h->didx, h->noise_sc, h->coop_ctr};
+                    h->rank_key, h->rank_idx, h->mbatch, h->mut_vec, h->dbuf, h->didx, h->noise_sc, h->coop_ctr,
+                    h->zero_noise, h->zero_idx, h->sens_tok};
+    if (h->sens) nicnes_sens_destroy(h->sens);
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (h->stats_pending) (void)hipEventSynchronize(h->stats_ev);
@@ -735,6 +742,7 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     // log-probs of a batch spread over several slabs: every slab runs to T, then the steps after the
     // batch's last finishing step are zeroed (nicnes_lp_batch_exit), as FCModel._sample leaves them
     p.no_exit = (p.lp && nslabs > 1) ? 1 : 0;
+    p.no_mask = 0;
     p.coop_ctr = h->coop_ctr;
     p.alive2 = h->alive + h->alive_stride;
     p.alive_stride = h->alive_stride;
@@ -803,6 +811,82 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
         HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
                                     h->fitness_mode, fitness_out, s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[2], s));
+    return NICNES_OK;
+}
+
+int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, float* out, void* stream) {
+    if (!h || !out || rows < 1) return NICNES_ERR_INVALID;
+    if (!h->theta_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_theta first");
+    if (!h->batch_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_batch first");
+    if (rows > h->B) return fail(h, NICNES_ERR_INVALID, "rows beyond the batch held");
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    const int L = 5, split = 100;                                  // forward_for_sensitivity defaults (nets.py:22)
+    if (!h->zero_noise) {
+        HIPC(h, hipDeviceSynchronize());
+        int rc = dalloc(h, &h->zero_noise, (size_t)h->D);
+        if (!rc) rc = dalloc(h, &h->zero_idx, 1);
+        if (!rc) rc = dalloc(h, &h->sens_tok, (size_t)2 * h->cfg.max_batch * (L - 1));
+        if (rc) return rc;
+        HIPC(h, hipMemset(h->zero_noise, 0, (size_t)h->D * sizeof(float)));
+        HIPC(h, hipMemset(h->zero_idx, 0, sizeof(uint64_t)));
+        h->sens = nicnes_sens_create();
+    }
+    // the greedy tokens of logit steps 1..L-1 from the engine's bit-exact decode of theta itself (sigma 0),
+    // every argmax fed back unmasked and no early exit, as forward_for_sensitivity runs (nets.py:48-64)
+    DecodeParams p;
+    p.theta = h->theta32;
+    p.noise = h->zero_noise;
+    p.noise_idx = h->zero_idx;
+    p.fc = h->fc;
+    p.member_batch = nullptr;
+    p.seq = h->sens_tok;
+    p.lp = nullptr;
+    p.scratch = h->dscratch;
+    p.stats = h->stats;
+    p.alive = h->alive;
+    p.alive2 = h->alive + h->alive_stride;
+    p.alive_stride = h->alive_stride;
+    p.part = h->part;
+    p.coop_ctr = h->coop_ctr;
+    p.coop = 0;
+    p.force_exact = h->force_exact;
+    p.lse_margin = h->lse_margin;
+    p.bounded_lse = 1;
+    p.no_exit = 1;
+    p.no_mask = 1;
+    p.B = rows;
+    p.F = h->cfg.fc_feat_size;
+    p.V1 = h->V1;
+    p.T = L - 1;
+    p.D = h->D;
+    p.G = 4;
+    p.S = 1;
+    p.off_img_w = h->off[0]; p.off_img_b = h->off[1]; p.off_emb_w = h->off[2]; p.off_log_w = h->off[3];
+    p.off_log_b = h->off[4]; p.off_i2h_w = h->off[5]; p.off_i2h_b = h->off[6]; p.off_h2h_w = h->off[7];
+    p.off_h2h_b = h->off[8];
+    HIPC(h, nicnes_launch_decode(&p, 1, nslabs_of(rows, 4), s, nullptr, nullptr, nullptr));
+    SensParams sp;
+    sp.theta = h->theta32;
+    sp.fc = h->fc;
+    sp.tok = h->sens_tok;                                          // member 0, sign +: [rows, L - 1]
+    sp.tok_stride = L - 1;
+    sp.Bs = rows;
+    sp.V1 = h->V1;
+    sp.E = h->cfg.input_encoding_size;
+    sp.R = h->cfg.rnn_size;
+    sp.F = h->cfg.fc_feat_size;
+    sp.L = L;
+    sp.split = split;
+    sp.K = h->V1 / split + 1;
+    sp.D = h->D;
+    sp.off_img_w = h->off[0]; sp.off_img_b = h->off[1]; sp.off_emb_w = h->off[2]; sp.off_log_w = h->off[3];
+    sp.off_log_b = h->off[4]; sp.off_i2h_w = h->off[5]; sp.off_i2h_b = h->off[6]; sp.off_h2h_w = h->off[7];
+    sp.off_h2h_b = h->off[8];
+    sp.underflow = underflow;
+    sp.out = out;
+    const int rc = nicnes_sens_run(h->sens, &sp, s);
+    if (rc) return fail(h, NICNES_ERR_HIP, "sensitivity kernels failed (code " + std::to_string(rc) + ")");
     return NICNES_OK;
 }
 

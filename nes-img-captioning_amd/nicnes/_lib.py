@@ -20,7 +20,7 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_set_decode_split', 'nicnes_decode_shape', 'nicnes_set_decode_streams', 'nicnes_comm_unique_id', 'nicnes_comm_init',
            'nicnes_comm_attach', 'nicnes_comm_destroy', 'nicnes_allgather_fitness', 'nicnes_allreduce_grad',
            'nicnes_noise_vectors', 'nicnes_set_batches', 'nicnes_evaluate_batches', 'nicnes_set_mutation',
-           'nicnes_set_decode_coop', 'nicnes_decode_path']
+           'nicnes_set_decode_coop', 'nicnes_decode_path', 'nicnes_sum_sensitivity']
 
 
 class NicnesConfig(ctypes.Structure):
@@ -82,6 +82,7 @@ def lib(path=None):
         'nicnes_set_decode_streams': (c.c_int, [vp, i32]),
         'nicnes_set_decode_coop': (c.c_int, [vp, i32]),
         'nicnes_decode_path': (c.c_int, [vp, i32, i32, vp]),
+        'nicnes_sum_sensitivity': (c.c_int, [vp, i32, f32, vp, vp]),
         'nicnes_comm_unique_id': (c.c_int, [vp]),
         'nicnes_comm_init': (c.c_int, [vp, i32, i32, vp]),
         'nicnes_comm_attach': (c.c_int, [vp, vp]),

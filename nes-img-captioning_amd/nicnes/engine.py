@@ -313,6 +313,16 @@ class Engine:
         Tokens do not depend on it."""
         check(self.L.nicnes_set_decode_streams(self.h, int(n)), self.h, 'set_decode_streams')
 
+    def sum_sensitivity(self, rows, underflow=0.0, out=None):
+        """SM-G-SUM sensitivity (Sensitivity.calc_sensitivity, safe_mutations.py:34-117) of the current theta
+        on the first `rows` images of the batch held: fp32 [D] on the GPU, clamped and scaled by
+        `underflow` when it is > 0 (the vector set_mutation('divide', ...) takes)."""
+        v = out if out is not None else torch.empty(self.D, dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_sum_sensitivity(self.h, int(rows), ctypes.c_float(underflow), _ptr(v), self._stream()),
+                  self.h, 'sum_sensitivity')
+        return v
+
     def set_decode_coop(self, mode=1):
         """1 (default): the split shape (128-row slabs, S = 2 or 4, every workgroup resident) runs as one
         persistent launch whose workgroups hand partial states and h' to each other; 0: two launches per

@@ -12,12 +12,12 @@ PolicyNet.evolve (src/algorithm/nets.py:83-119) transforms the member's noise be
 
 The engine applies the transform on the GPU (nicnes_set_mutation: one prepass materialises
 fp32(fp32(sigma * z) / s) or fp32(fp32(sigma * z) * |theta'|) per member, which the decode, the
-weighted noise sum and nicnes_noise_vectors then read). This module computes the per-parameter
-vector s on the host once per task, as the reference's workers do (nic_nes_worker.py:137-140):
-the sensitivity is a Jacobian of 95 grouped log-prob outputs after 5 greedy steps
-(CaptionModel.forward_for_sensitivity, src/captioning/nets.py:22-70) -- 95 backward passes of a
-5-step decode on at most orig_batch_size images, taken with torch autograd on the CPU in the
-reference's own op order, so the vector is the reference's vector.
+weighted noise sum and nicnes_noise_vectors then read). The SM-G-SUM vector s is computed once per
+task, as the reference's workers do (nic_nes_worker.py:137-140), by the engine itself
+(Engine.sum_sensitivity -> nicnes_sum_sensitivity: the Jacobian of 95 grouped log-prob outputs after 5
+greedy steps, CaptionModel.forward_for_sensitivity, src/captioning/nets.py:22-70, its 95 backward
+passes batched on the GPU); oracle/sensitivity_ref.py keeps the torch-autograd restatement in the
+reference's op order that pins it (bit-exact vs the reference's calc_sensitivity).
 
 One sensitivity per task: the reference caches it per (task, parent 0) in a file shared by the
 workers (safe_mutations.py:34-52), so every member uses the first worker's batch; with
@@ -25,93 +25,9 @@ single_batch: false the engine uses the iteration's first batch for it (batch 0)
 """
 import numpy as np
 import torch
-import torch.nn as nn
-import torch.nn.functional as F
 
 SAFE_DIVIDE = ('SM-G-SUM', 'SM-VECTOR')
 MODES = ('', 'SM-G-SUM', 'SM-G-ABS', 'SM-VECTOR', 'SM-PROPORTIONAL')
-
-
-class _Core(nn.Module):
-    """LSTMCore without vbn / layer norm (src/captioning/nets.py:75-134)."""
-
-    def __init__(self, E, R):
-        super().__init__()
-        self.R = R
-        self.i2h = nn.Linear(E, 5 * R)
-        self.h2h = nn.Linear(R, 5 * R)
-
-    def forward(self, xt, h, c):
-        s = self.i2h(xt) + self.h2h(h)
-        g = torch.sigmoid(s.narrow(1, 0, 3 * self.R))
-        ig, fg, og = g.narrow(1, 0, self.R), g.narrow(1, self.R, self.R), g.narrow(1, 2 * self.R, self.R)
-        tr = torch.max(s.narrow(1, 3 * self.R, self.R), s.narrow(1, 4 * self.R, self.R))
-        c = fg * c + ig * tr
-        return og * torch.tanh(c), c
-
-
-class SensitivityNet(nn.Module):
-    """The fc_caption parameters in FCModel registration order (nets.py:150-153), differentiable,
-    for the sensitivity Jacobian only (the engine's decode runs on the GPU)."""
-
-    def __init__(self, V1, E, R, F_):
-        super().__init__()
-        self.R = R
-        self.img_embed = nn.Linear(F_, E)
-        self.embed = nn.Embedding(V1, E)
-        self.logit = nn.Linear(R, V1)
-        self.core = _Core(E, R)
-
-    def load_vector(self, theta32):
-        nn.utils.vector_to_parameters(torch.as_tensor(np.asarray(theta32, np.float32)), self.parameters())
-
-    def forward_for_sensitivity(self, fc_unique, orig_bs=0, split=100, length=5):
-        """captioning/nets.py:22-70 on unique image rows: log-probs after `length` greedy steps, the
-        vocabulary zero-padded to a multiple of `split` and each group reduced to its 2-norm."""
-        fc = torch.as_tensor(np.ascontiguousarray(fc_unique, np.float32))
-        if fc.size(0) > orig_bs > 0:
-            fc = fc[:orig_bs]
-        B = fc.size(0)
-        h = fc.new_zeros(B, self.R)
-        c = fc.new_zeros(B, self.R)
-        h, c = self.core(self.img_embed(fc), h, c)
-        it = torch.zeros(B, dtype=torch.long)
-        for _ in range(length):
-            h, c = self.core(self.embed(it), h, c)
-            logprobs = F.log_softmax(self.logit(h), dim=1)
-            _, it = torch.max(logprobs.data, 1)
-            it = it.view(-1).long()
-        pad = split - (logprobs.size(1) % split)
-        ext = torch.cat((logprobs, torch.zeros((B, pad))), 1)
-        return ((torch.stack(ext.split(split, dim=1)) ** 2).sum(2) ** (1 / 2)).permute(1, 0)
-
-    def extract_grad(self):
-        return torch.cat([p.grad.data.flatten() for p in self.parameters()])
-
-
-def sum_sensitivity(dims, theta32, fc_unique, orig_bs):
-    """Sensitivity._calc_sum_sensitivity (safe_mutations.py:86-110): per parameter, the 2-norm over
-    the grouped outputs of d(output summed over the batch)/d(theta), divided by the batch size.
-    dims = (V1, E, R, F). Returns fp32 [D] (before the underflow clamp)."""
-    net = SensitivityNet(*dims)
-    net.load_vector(theta32)
-    with torch.enable_grad():
-        for p in net.parameters():
-            p.requires_grad_(True)
-        out = net.forward_for_sensitivity(fc_unique, orig_bs)
-        n_out, B = out.size(1), out.size(0)
-        D = sum(p.numel() for p in net.parameters())
-        jac = torch.zeros(n_out, D)
-        go = torch.zeros(*out.size())
-        for k in range(n_out):
-            net.zero_grad()
-            go.zero_()
-            go[:, k] = 1.0
-            out.backward(gradient=go, retain_graph=True)
-            jac[k] = net.extract_grad()
-    s = torch.sqrt((jac ** 2).sum(0))
-    s /= B
-    return s.detach()
 
 
 def clamp_calc(s, underflow):
@@ -152,10 +68,11 @@ def proportional_vector(theta32):
 class Mutator:
     """Sets the engine's noise transform for each task (nets.py:83-119 semantics).
 
-    prepare(key, theta32, fc_unique) is called with the task's fp32 theta and its (first) batch's
-    unique fc rows before the task's members are evaluated or summed; the vector is recomputed only
-    when `key` changes. Workers and the master compute the same vector from the same inputs (CPU
-    torch, deterministic), so the master's weighted noise sum uses the workers' noise."""
+    prepare(key, theta32, fc_unique) is called with the task's fp32 theta (loaded in the engine) and its
+    (first) batch's unique fc rows (the batch the engine holds) before the task's members are evaluated
+    or summed; the vector is recomputed only when `key` changes. Workers and the master compute the
+    vector from the same inputs with the same engine code, so the master's weighted noise sum uses the
+    workers' noise."""
 
     def __init__(self, spec, engine):
         mo = spec.model_options
@@ -163,8 +80,6 @@ class Mutator:
         self.e = engine
         self.underflow = float(mo.safe_mutation_underflow or 0.0)
         self.orig_bs = spec.batch_size                   # Experiment.orig_batch_size (experiment.py:29,110)
-        c = engine.cfg
-        self.dims = (c.vocab_size + 1, c.input_encoding_size, c.rnn_size, c.fc_feat_size)
         self._key = None
         self.vector = None
         if self.mode == 'SM-VECTOR':
@@ -186,8 +101,13 @@ class Mutator:
             self.vector = proportional_vector(th)
             self.e.set_mutation('scale', self.vector)
         else:
-            s = sum_sensitivity(self.dims, th, fc_unique, self.orig_bs)
-            self.vector = clamp_calc(s, self.underflow)
+            if not self.underflow > 0:
+                raise ValueError('SM-G-SUM needs safe_mutation_underflow > 0 (the reference divides by it)')
+            # forward_for_sensitivity's rows: the batch's unique images, the first orig_batch_size of them
+            rows = int(np.asarray(fc_unique).shape[0])
+            if rows > self.orig_bs > 0:
+                rows = self.orig_bs
+            self.vector = self.e.sum_sensitivity(rows, self.underflow)
             self.e.set_mutation('divide', self.vector)
         self._key = key
         return self.vector

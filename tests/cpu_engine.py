@@ -31,6 +31,16 @@ class OracleEngine:
         v = vec.numpy() if isinstance(vec, torch.Tensor) else vec
         self.mutation = None if mode == 'plain' else (mode, np.asarray(v, np.float32).copy())
 
+    def sum_sensitivity(self, rows, underflow=0.0):
+        """nicnes_sum_sensitivity on the CPU: the torch-autograd oracle (oracle/sensitivity_ref.py) on the
+        first `rows` images of the batch held."""
+        from nicnes.mutations import clamp_calc
+        from oracle import sensitivity_ref as SR
+        d = self.dims
+        fc = self.batches[0][0] if getattr(self, 'batches', None) else np.asarray(self.fc)   # batch 0
+        s = SR.sum_sensitivity((d.vocab_size + 1, d.E, d.R, d.F), self.theta32, fc[:rows], rows)
+        return clamp_calc(s, underflow) if underflow > 0 else s
+
     def set_fitness_mode(self, fitness):
         self.fitness_mode = CR.CRITERIA[fitness] if isinstance(fitness, str) else int(fitness)
 

@@ -399,13 +399,14 @@ def _mut_spec(P, mode, **mo):
 
 
 def test_mutation_goldens_from_the_reference():
-    """tests/golden/mutations.npz (scripts/make_golden.py, the reference's FCModel): the host SM-G-SUM
-    sensitivity equals Sensitivity.calc_sensitivity bit for bit; the oracle's transform of a noise draw
+    """tests/golden/mutations.npz (scripts/make_golden.py, the reference's FCModel): the oracle's SM-G-SUM
+    sensitivity (oracle/sensitivity_ref.py) equals Sensitivity.calc_sensitivity bit for bit; the oracle's transform of a noise draw
     equals PolicyNet.evolve's returned noise for SM-G-SUM and SM-PROPORTIONAL."""
     from nicnes import mutations as MU
+    from oracle import sensitivity_ref as SR
     g = np.load('tests/golden/mutations.npz')
     V, E, R, F_ = [int(x) for x in g['dims']]
-    s = MU.clamp_calc(MU.sum_sensitivity((V + 1, E, R, F_), g['theta'], g['fc'], 4), float(g['underflow']))
+    s = MU.clamp_calc(SR.sum_sensitivity((V + 1, E, R, F_), g['theta'], g['fc'], 4), float(g['underflow']))
     assert np.array_equal(s.numpy(), g['sensitivity'])
     raw = g['raw']
     D = raw.size
