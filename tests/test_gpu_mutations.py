@@ -109,6 +109,7 @@ def test_gpu_sensitivity_matches_oracle(theta_kind, rows):
     try:
         e.set_noise_table(O.noise_table(NOISE_LEN, 123))
         e.set_theta(theta)
+        e.set_df_table(np.zeros(0, np.uint64), np.zeros(0), np.log(64.0))
         e.set_batch(fc, [np.zeros((1, dims.T), np.int32)] * fc.shape[0])
         raw = e.sum_sensitivity(rows).cpu().numpy()
         clamped = e.sum_sensitivity(rows, 0.1).cpu().numpy()
