@@ -257,9 +257,11 @@ def main():
         fc_rows = wl['fc'][:B]
 
         def prepare(it_):
-            t_ = time.perf_counter()
-            mutator.prepare(it_, eng.theta()[1], fc_rows)
-            mut_s.append(time.perf_counter() - t_)
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            mutator.prepare(it_, eng.theta()[1], fc_rows)       # SM-G-SUM: enqueued on the engine's stream
+            ev1.record()
+            mut_s.append((ev0, ev1))
     else:
         def prepare(it_):
             pass
@@ -292,6 +294,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     value = P * args.steps / dt
+    mut_ms = float(np.mean([a.elapsed_time(b) for a, b in mut_s])) if mut_s else 0.0
     dec_s = float(np.mean(dec_ms)) / 1e3
     flops = decode_flops_per_member(B) * P_local
     # dominant kernel: the fused steps kernel (logits + token + next LSTM cell for every step t = -1..T,
@@ -385,10 +388,11 @@ def main():
         'cpu_baseline': cpu,
         'decodes_per_s': round(2 * value, 3),        # one decode = one sign's rollout of the batch
         'tie_fallbacks': eng.stats()['tie_fallbacks'],
-        'mutation': ({'mode': args.mutation, 'host_vector_s_per_iteration': round(float(np.mean(mut_s)), 4),
-                      'host_share_of_iteration': round(float(np.sum(mut_s)) / dt, 4),
-                      'note': 'the per-task mutation vector on the host CPU (torch autograd for SM-G-SUM: 95 '
-                              'backward passes of a 5-step decode, safe_mutations.py:93-117)'}
+        'mutation': ({'mode': args.mutation, 'vector_ms_per_iteration': round(mut_ms, 3),
+                      'vector_share_of_iteration': round(mut_ms / (dt / args.steps * 1e3), 4),
+                      'note': 'the per-task mutation vector, timed with events on the engine stream: SM-G-SUM '
+                              '= nicnes_sum_sensitivity (the sigma 0 token decode + 95 batched backward passes of '
+                              'a 5-step decode, safe_mutations.py:93-117), SM-PROPORTIONAL = |theta| on the host'}
                      if args.mutation else None),
         'update_ratio': ratio,
     }

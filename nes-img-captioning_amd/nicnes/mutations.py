@@ -95,10 +95,9 @@ class Mutator:
     def prepare(self, key, theta32, fc_unique):
         if not self.active or key == self._key:
             return self.vector
-        th = theta32.detach().cpu().numpy() if isinstance(theta32, torch.Tensor) else np.asarray(theta32)
-        th = th.astype(np.float32, copy=False)
         if self.mode == 'SM-PROPORTIONAL':
-            self.vector = proportional_vector(th)
+            th = theta32.detach().cpu().numpy() if isinstance(theta32, torch.Tensor) else np.asarray(theta32)
+            self.vector = proportional_vector(th.astype(np.float32, copy=False))
             self.e.set_mutation('scale', self.vector)
         else:
             if not self.underflow > 0:
