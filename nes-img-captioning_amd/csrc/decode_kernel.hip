@@ -78,6 +78,9 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef LOGIT_MID_AT
 #define LOGIT_MID_AT 6     // ... before half-chunk LOGIT_MID_AT of 8 (measured: 5-7 equal, 2 and 8 -0.8 %)
 #endif
+#ifndef COOP_SC1
+#define COOP_SC1 1         // coop path: handed-off partials and h' read with sc1 loads instead of an agent acquire
+#endif
 #ifndef DECODE_PRIO
 #define DECODE_PRIO 0      // s_setprio 1 for one half of the workgroup's waves: 1 = waves 4-7, 2 = waves 0-3
 #endif
@@ -136,6 +139,10 @@ __device__ __forceinline__ f32x4 ld4(rsrc_t r, uint32_t byte_off, uint32_t soff 
 }
 __device__ __forceinline__ float ld1(rsrc_t r, uint32_t byte_off, uint32_t soff = 0) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, (int)soff, 0));
+}
+// sc1 load (bypasses this CU's L1): a handed-off word read without an agent acquire (coop path)
+__device__ __forceinline__ float ld1_sc1(rsrc_t r, uint32_t byte_off, uint32_t soff = 0) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, (int)soff, 16));
 }
 __device__ __forceinline__ void st1(rsrc_t r, uint32_t byte_off, uint32_t soff, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)byte_off, (int)soff, 0);
@@ -1684,7 +1691,10 @@ __device__ __forceinline__ void coop_arrive(uint32_t* ctr) {
 }
 
 // false (for every thread) when the partners have not arrived within COOP_SPIN_TICKS: the launch then
-// ends early and stats[2] counts it (the engine reports it as an error)
+// ends early and stats[2] counts it (the engine reports it as an error). ACQ: one agent acquire after the
+// poll (plain loads of the handed-off bytes may follow); without it every such load must be an sc1 load
+// (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 hand-off table)
+template <bool ACQ = true>
 __device__ __forceinline__ bool coop_wait(uint32_t* ctr, uint32_t target, int32_t* stats) {
     int bad = 0;
     if (threadIdx.x == 0) {
@@ -1698,10 +1708,11 @@ __device__ __forceinline__ bool coop_wait(uint32_t* ctr, uint32_t target, int32_
             }
         }
     }
-    if (threadIdx.x < 64) {
+    if (ACQ && threadIdx.x < 64) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    if (!ACQ) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: the loads stay below the poll
     return __syncthreads_or(bad) == 0;
 }
 
@@ -1769,7 +1780,7 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         coop_arrive(ctr);
         ++phase;
 #if !(DECODE_ABLATE & 128)
-        if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
+        if (!coop_wait<!COOP_SC1>(ctr, (uint32_t)S * phase, p.stats)) return false;
 #endif
         PROF_AT(blockIdx.x, 1024, pm + 2);
         float m = 0.f, lse = 0.f;
@@ -1777,10 +1788,32 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         bool ovf = false;
         {
             Part8 pr;
+#if COOP_SC1
+            {   // the S partial states of this wave's rows, sc1 loads (written sc1 by the group)
+                const uint32_t po = 4u * (uint32_t)(c.wave * (7 * 64) + lane_fresh());
+#pragma unroll
+                for (int u = 0; u < S; ++u) {
+                    const rsrc_t r = make_rsrc(part_ptr(p, c.wg, u, 0), PART_FLOATS * 4);
+                    pr.m[u] = ld1_sc1(r, po, 0u); pr.s[u] = ld1_sc1(r, po, 256u);
+                    pr.r0v[u] = ld1_sc1(r, po, 512u); pr.r0i[u] = __builtin_bit_cast(int, ld1_sc1(r, po, 768u));
+                    pr.r1v[u] = ld1_sc1(r, po, 1024u); pr.r1i[u] = __builtin_bit_cast(int, ld1_sc1(r, po, 1280u));
+                    pr.ev[u] = ld1_sc1(r, po, 1536u);
+                }
+            }
+#else
             load_part8(p, c.wg, c.wave, lane_fresh(), 1, S, 0, pr);
+#endif
             merge_partials(p, c.wg, c.wave, lane_fresh(), 1, S, pr, PAIRS, m, lse, tok, ovf);
         }
         if (__syncthreads_or((p.force_exact || ovf) ? 1 : 0)) {
+#if COOP_SC1
+            // the exact pass re-reads the partials with plain loads: acquire them first (rare path)
+            if (threadIdx.x < 64) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+#endif
             // the exact sweep stages through LDS with registers of its own: the prefetched cell tile is
             // given up (reloaded below)
             merge_exact(p, lds, c.wg, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.wave, c.lane, 1, S, hB, true,
@@ -1889,11 +1922,11 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
     coop_arrive(ctr);
     ++phase;
 #if !(DECODE_ABLATE & 128)
-    if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
+    if (!coop_wait<!COOP_SC1>(ctr, (uint32_t)S * phase, p.stats)) return false;
 #endif
     PROF_AT(blockIdx.x, 1024, pm + 5);
 #pragma unroll
-    for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, HP_SLOT(hpar, i));
+    for (int i = 0; i < 64; ++i) hB[i] = COOP_SC1 ? ld1_sc1(c.scr_r, lo, HP_SLOT(hpar, i)) : ld1(c.scr_r, lo, HP_SLOT(hpar, i));
     return true;
 }
 
