@@ -79,7 +79,7 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #define LOGIT_MID_AT 6     // ... before half-chunk LOGIT_MID_AT of 8 (measured: 5-7 equal, 2 and 8 -0.8 %)
 #endif
 #ifndef COOP_SC1
-#define COOP_SC1 1         // coop path: handed-off partials and h' read with sc1 loads instead of an agent acquire
+#define COOP_SC1 0         // coop path: 1 = handed-off partials and h' read with sc1 loads instead of an agent acquire (measured: equal at P = 64, 0.6 % slower at P = 128)
 #endif
 #ifndef DECODE_PRIO
 #define DECODE_PRIO 0      // s_setprio 1 for one half of the workgroup's waves: 1 = waves 4-7, 2 = waves 0-3
