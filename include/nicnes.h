@@ -159,6 +159,10 @@ int nicnes_rank_weights(nicnes_handle* h, const double* fitness, int32_t P, doub
  * and nicnes_adam_step. */
 int nicnes_grad_partial(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, const float* w,
                         float sigma, float* gsum_out, void* stream);
+/* The same sum on parameters [j0, j1) only (j0 a multiple of 64): gsum_out[j0 .. j1) written. Lets a
+ * multi-GPU caller all-reduce one range while the next is summed (not a reference interface). */
+int nicnes_grad_partial_range(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, const float* w,
+                              float sigma, int64_t j0, int64_t j1, float* gsum_out, void* stream);
 
 /* g = gsum / (2P); globalg = -g + l2coeff * theta; Adam step on the engine's theta
  * (nic_nes_master.py:126-137, optimizers.py:15-22,78-83). With ratio_out_host set it is

@@ -926,6 +926,22 @@ int nicnes_grad_partial(nicnes_handle* h, uint64_t iteration, int32_t member_beg
     return NICNES_OK;
 }
 
+int nicnes_grad_partial_range(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, const float* w,
+                              float sigma, int64_t j0, int64_t j1, float* gsum_out, void* stream) {
+    if (!h || !w || !gsum_out || member_begin < 0 || count < 0) return NICNES_ERR_INVALID;
+    if (j0 < 0 || j1 > h->D || j0 >= j1 || (j0 & 63)) return fail(h, NICNES_ERR_INVALID, "range: 0 <= j0 < j1 <= D, j0 % 64 == 0");
+    if (count > h->cfg.max_members) return fail(h, NICNES_ERR_INVALID, "count > max_members");
+    if (!h->noise) return fail(h, NICNES_ERR_INVALID, "nicnes_set_noise_table first");
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, nicnes_launch_noise_index(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, h->cfg.noise_len,
+                                      (uint64_t)h->D, h->nidx, s));
+    // the same kernel on the parameter range (slices are 64-float aligned, so j0 % 64 keeps the f32x4 loads aligned)
+    HIPC(h, nicnes_launch_grad(h->noise + j0, h->nidx, w, count, sigma, j1 - j0, h->mut_vec ? h->mut_vec + j0 : nullptr,
+                               h->mut_mode, gsum_out + j0, s));
+    return NICNES_OK;
+}
+
 // one optimizer update (kind 0 Adam, 1 SGD), from the fused NES form (gsum, P, l2coeff) or from a
 // given globalg (Optimizer.update(globalg), optimizers.py:15-22)
 static int opt_step(nicnes_handle* h, int kind, const float* gsum, int32_t P, double l2coeff, const double* globalg,

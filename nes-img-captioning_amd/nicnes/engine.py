@@ -248,6 +248,14 @@ class Engine:
                                              ctypes.c_float(sigma), _ptr(g), self._stream()), self.h, 'grad_partial')
         return g
 
+    def grad_partial_range(self, iteration, member_begin, count, w_shard, sigma, j0, j1, out):
+        """grad_partial on parameters [j0, j1) of `out` (j0 a multiple of 64)."""
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_grad_partial_range(self.h, ctypes.c_uint64(iteration), member_begin, count,
+                                                   _ptr(w_shard), ctypes.c_float(sigma), int(j0), int(j1), _ptr(out),
+                                                   self._stream()), self.h, 'grad_partial_range')
+        return out
+
     def adam_step(self, gsum, P, l2coeff, stepsize, beta1=0.9, beta2=0.999, epsilon=1e-08, sync=True):
         """Adam on the engine's theta. sync=True returns the update ratio (one host sync); sync=False
         only enqueues the step and returns None (read the ratio later with last_ratio())."""

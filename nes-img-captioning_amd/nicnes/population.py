@@ -16,8 +16,12 @@ import torch.distributed as dist
 
 
 class PopulationRunner:
+    """overlap_chunks (torch.distributed exchange, world > 1): the noise sum is computed in that many
+    parameter ranges, each range's all-reduce running on the collective stream while the next range is
+    summed, so the 11.46 MB all-reduce hides behind the sum instead of following it."""
+
     def __init__(self, engine, population, sigma, l2coeff=0.0, stepsize=1e-3, beta1=0.9, beta2=0.999,
-                 epsilon=1e-08, rank=0, world_size=1, group=None, comm=None):
+                 epsilon=1e-08, rank=0, world_size=1, group=None, comm=None, overlap_chunks=4):
         assert population % world_size == 0, 'population must split evenly over ranks'
         self.e = engine
         self.P = population
@@ -34,6 +38,11 @@ class PopulationRunner:
         self.fit_local = torch.empty((self.local, 2), dtype=torch.float64, device=dev)
         self.fit_all = torch.empty((self.P, 2), dtype=torch.float64, device=dev) if world_size > 1 else self.fit_local
         self.gsum = torch.empty(engine.D, dtype=torch.float32, device=dev)
+        D = engine.D
+        n = max(1, int(overlap_chunks)) if (world_size > 1 and comm is None and
+                                             hasattr(engine, 'grad_partial_range')) else 1
+        cuts = [0] + [min(D, (D * k // n + 63) // 64 * 64) for k in range(1, n)] + [D]
+        self.ranges = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
 
     def evaluate(self, iteration, n_batches=1):
         """this rank's members -> fitness [local, 2] (f+, f-). With n_batches > 1 (the engine holds
@@ -65,9 +74,19 @@ class PopulationRunner:
         """ranks -> weighted noise sum (local members) -> all-reduce -> Adam. Returns the update ratio
         (sync=False: nothing waits for the GPU and None is returned; engine.last_ratio() reads it)."""
         _, w = self.e.rank_weights(self.fit_all)
-        self.e.grad_partial(iteration, self.m0, self.local, w[self.m0:self.m0 + self.local], self.sigma,
-                            out=self.gsum)
-        self.reduce_noise_sum()
+        w_local = w[self.m0:self.m0 + self.local]
+        if len(self.ranges) > 1:
+            # range k's all-reduce (collective stream) overlaps the sum of range k + 1 (compute stream)
+            works = []
+            for j0, j1 in self.ranges:
+                self.e.grad_partial_range(iteration, self.m0, self.local, w_local, self.sigma, j0, j1, self.gsum)
+                works.append(dist.all_reduce(self.gsum[j0:j1], op=dist.ReduceOp.SUM, group=self.group,
+                                             async_op=True))
+            for wk in works:
+                wk.wait()
+        else:
+            self.e.grad_partial(iteration, self.m0, self.local, w_local, self.sigma, out=self.gsum)
+            self.reduce_noise_sum()
         return self.e.adam_step(self.gsum, self.P, self.l2coeff, self.stepsize, self.beta1, self.beta2,
                                 self.epsilon, sync=sync)
 

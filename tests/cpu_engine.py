@@ -116,6 +116,11 @@ class OracleEngine:
             return out
         return g
 
+    def grad_partial_range(self, iteration, member_begin, count, w_shard, sigma, j0, j1, out):
+        g = self.grad_partial(iteration, member_begin, count, w_shard, sigma)
+        out[j0:j1] = g[j0:j1]
+        return out
+
     def adam_step(self, gsum, P, l2coeff, stepsize, beta1=0.9, beta2=0.999, epsilon=1e-08, sync=True):
         if self.adam is None:
             self.adam = O.AdamOracle(self.theta_src.copy(), stepsize, beta1, beta2, epsilon)

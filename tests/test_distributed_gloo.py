@@ -23,18 +23,21 @@ def _free_port():
     return p
 
 
-def _run(rank, world, port, out_dir):
+def _run(rank, world, port, out_dir, chunks=4):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     if world > 1:
         dist.init_process_group('gloo', rank=rank, world_size=world)
     eng = OracleEngine(*tiny_workload())
-    r = PopulationRunner(eng, P, SIGMA, l2coeff=1e-3, stepsize=1e-2, rank=rank, world_size=world)
+    r = PopulationRunner(eng, P, SIGMA, l2coeff=1e-3, stepsize=1e-2, rank=rank, world_size=world,
+                         overlap_chunks=chunks)
+    if world > 1:
+        assert len(r.ranges) == min(chunks, len(r.ranges)) and r.ranges[0][0] == 0 and r.ranges[-1][1] == eng.D
     fits = []
     for it in range(1, ITERS + 1):
         f, ratio = r.step(it)
         fits.append(f.clone().numpy())
-    np.savez(os.path.join(out_dir, 'r%d_w%d.npz' % (rank, world)), fits=np.stack(fits), theta=eng.theta32)
+    np.savez(os.path.join(out_dir, 'r%d_w%d_c%d.npz' % (rank, world, chunks)), fits=np.stack(fits), theta=eng.theta32)
     if world > 1:
         dist.destroy_process_group()
 
@@ -42,14 +45,24 @@ def _run(rank, world, port, out_dir):
 def test_two_rank_gloo_matches_single_rank(tmp_path):
     _run(0, 1, _free_port(), str(tmp_path))
     mp.spawn(_run, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    one = np.load(tmp_path / 'r0_w1.npz')
+    one = np.load(tmp_path / 'r0_w1_c4.npz')
     for rank in range(2):
-        two = np.load(tmp_path / ('r%d_w2.npz' % rank))
+        two = np.load(tmp_path / ('r%d_w2_c4.npz' % rank))
         assert np.array_equal(one['fits'], two['fits'])
         assert np.allclose(one['theta'], two['theta'], rtol=0, atol=1e-6)
     # both ranks hold the identical replicated theta
-    a, b = np.load(tmp_path / 'r0_w2.npz'), np.load(tmp_path / 'r1_w2.npz')
+    a, b = np.load(tmp_path / 'r0_w2_c4.npz'), np.load(tmp_path / 'r1_w2_c4.npz')
     assert np.array_equal(a['theta'], b['theta'])
+
+
+def test_overlapped_range_all_reduce_equals_one_all_reduce(tmp_path):
+    """The noise sum in parameter ranges, each all-reduced while the next is summed (overlap_chunks), gives
+    the same theta as one sum and one all-reduce."""
+    for chunks in (1, 3):
+        mp.spawn(_run, args=(2, _free_port(), str(tmp_path), chunks), nprocs=2, join=True)
+    for rank in range(2):
+        a, b = np.load(tmp_path / ('r%d_w2_c1.npz' % rank)), np.load(tmp_path / ('r%d_w2_c3.npz' % rank))
+        assert np.array_equal(a['fits'], b['fits']) and np.array_equal(a['theta'], b['theta'])
 
 
 def _run_master(rank, world, port, out_dir):

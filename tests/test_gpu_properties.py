@@ -83,6 +83,19 @@ def test_noise_sum_sign_and_scale_linearity(eng):
     assert float((g_a + g_b - g.double()).abs().max()) <= tol
 
 
+def test_noise_sum_in_ranges_equals_whole(eng):
+    """nicnes_grad_partial_range over 64-aligned cuts of [0, D) rebuilds grad_partial bit for bit (the
+    ranges population.py all-reduces while the next one is summed)."""
+    P, it = 12, 9
+    w = torch.from_numpy(np.random.default_rng(4).standard_normal(P).astype(np.float32)).cuda()
+    g = eng.grad_partial(it, 0, P, w, SIGMA)
+    cuts = [0, 64 * 3, 64 * 1000, (eng.D // 2) // 64 * 64, eng.D]
+    out = torch.full_like(g, float('nan'))
+    for j0, j1 in zip(cuts[:-1], cuts[1:]):
+        eng.grad_partial_range(it, 0, P, w, SIGMA, j0, j1, out)
+    assert torch.equal(out, g)
+
+
 @pytest.mark.parametrize('B,bu', [(130, False), (40, True)], ids=['two_slabs', 'bu_features'])
 def test_tokens_match_oracle(eng, B, bu):
     dims = O.Dims()
