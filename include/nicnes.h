@@ -147,6 +147,16 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
                             const int32_t* member_batch_host, double* fitness_out, int32_t* seq_out, float* logprob_out,
                             void* stream);
 
+/* CaptPolicy.rollout of theta itself (src/captioning/policies.py:86-128, called for the eval result
+ * of nic_nes_worker.py:65-70 with the unperturbed parameters): fitness_out[0] = the fitness of the
+ * batch (the one held, or batch `batch` of nicnes_set_batches), decoded ONCE. At sigma = 0 both
+ * antithetic signs are theta, so sign + decodes the first ceil(B/2) images and sign - the rest and
+ * the halves are scored as one rollout: seq_out [B, seq_length] int32 and logprob_out [B, seq_length]
+ * (both nullable, rows 0..B-1 in batch order) and the fitness equal nicnes_evaluate_lp's sign-+
+ * row of a sigma = 0 member bit for bit, at half its decode work. */
+int nicnes_evaluate_theta(nicnes_handle* h, int32_t batch, double* fitness_out, int32_t* seq_out, float* logprob_out,
+                          void* stream);
+
 /* Centred ranks + antithetic weights over the WHOLE population, replaces
  * NESMaster.compute_centered_ranks and the weights line of gradient_estimate
  * (src/algorithm/nic_nes/nic_nes_master.py:170-205). fitness [P, 2] fp64 -> cr [P, 2] (or NULL),

@@ -849,6 +849,12 @@ struct Ctx {
     rsrc_t theta_r, noise_r, scr_r;
 };
 
+// a row is decoded when it lies in the slab range and its image in the batch (sign_off > 0: sign 1 takes the
+// second half of the images, DecodeParams::sign_off)
+__device__ __forceinline__ bool row_ok(const DecodeParams& p, int b, int sgn) {
+    return b < p.B && b + sgn * p.sign_off < p.B_img;
+}
+
 __device__ __forceinline__ Ctx make_ctx(const DecodeParams& p) {
     Ctx c;
     c.tid = threadIdx.x;
@@ -861,7 +867,7 @@ __device__ __forceinline__ Ctx make_ctx(const DecodeParams& p) {
     c.slab = blockIdx.y;
     c.wg = c.member * gridDim.y + c.slab;
     c.b = c.slab * 128 + c.grp * 32 + (c.lane & 31);
-    c.row_valid = c.b < p.B;
+    c.row_valid = row_ok(p, c.b, c.sgn);
     c.bc = c.row_valid ? c.b : 0;
     const uint64_t nidx = p.noise_idx[c.member];
     const uint32_t Dbytes = 4u * (uint32_t)p.D;
@@ -899,7 +905,7 @@ __device__ __forceinline__ SCtx<G> make_sctx(const DecodeParams& p) {
     c.slab = blockIdx.z;
     c.wg = c.member * gridDim.z + c.slab;
     c.b = c.slab * (32 * G) + c.grp * 32 + (c.lane & 31);
-    c.row_valid = c.b < p.B;
+    c.row_valid = row_ok(p, c.b, c.sgn);
     c.bc = c.row_valid ? c.b : 0;
     const uint64_t nidx = p.noise_idx[c.member];
     const uint32_t Dbytes = 4u * (uint32_t)p.D;
@@ -920,8 +926,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
     const SCtx<G> c = make_sctx<G>(p);
     const bool fused_path = G == 4 && p.S == 1;
     if (fused_path) PROF_MARK(80); else PROF_SPLIT(250);
-    const float* fcm = p.fc + (p.member_batch ? (size_t)p.member_batch[c.member] * p.B * p.F : 0);
-    const rsrc_t fc_r = make_rsrc(fcm, 4u * (uint32_t)p.B * (uint32_t)p.F);
+    const float* fcm = p.fc + (p.member_batch ? (size_t)p.member_batch[c.member] * p.B_img * p.F : 0);
+    const rsrc_t fc_r = make_rsrc(fcm, 4u * (uint32_t)p.B_img * (uint32_t)p.F);
+    const int fr = c.row_valid ? c.b + c.sgn * p.sign_off : 0;      // the lane's fc row
     const uint32_t lo = 4u * c.lane;
     const bool mm = G == 4 || c.hf == 0;
     StageRegs sr;
@@ -939,7 +946,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
     stage_store(lds, desc(0), c.tid, sr);
     __syncthreads();
     for (int kc = 0; kc < nK; ++kc) {
-        const uint32_t frow = 4u * (uint32_t)(c.bc * p.F + 128 * kc + 4 * c.hh);
+        const uint32_t frow = 4u * (uint32_t)(fr * p.F + 128 * kc + 4 * c.hh);
 #pragma unroll
         for (int U = 0; U < 4; ++U) {
             if (U < nb) {
@@ -978,8 +985,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img64_kernel(DecodePar
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const Ctx c = make_ctx(p);
     PROF_MARK(80);
-    const float* fcm = p.fc + (p.member_batch ? (size_t)p.member_batch[c.member] * p.B * p.F : 0);
-    const rsrc_t fc_r = make_rsrc(fcm, 4u * (uint32_t)p.B * (uint32_t)p.F);
+    const float* fcm = p.fc + (p.member_batch ? (size_t)p.member_batch[c.member] * p.B_img * p.F : 0);
+    const rsrc_t fc_r = make_rsrc(fcm, 4u * (uint32_t)p.B_img * (uint32_t)p.F);
+    const int fr = c.row_valid ? c.b + c.sgn * p.sign_off : 0;      // the lane's fc row
     const int nK = p.F >> 7;
     const uint32_t F = (uint32_t)p.F;
     auto load = [&](int j, Stage64Regs& r) __attribute__((always_inline)) {
@@ -997,7 +1005,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img64_kernel(DecodePar
         r.bz = ld1(c.noise_r, bo);
     };
     auto load_fc = [&](int kc, float (&dst)[64]) __attribute__((always_inline)) {
-        const uint32_t frow = 4u * ((uint32_t)c.bc * F + 128u * (uint32_t)kc + 4u * (uint32_t)c.hh);
+        const uint32_t frow = 4u * ((uint32_t)fr * F + 128u * (uint32_t)kc + 4u * (uint32_t)c.hh);
 #pragma unroll
         for (int T = 0; T < 4; ++T)
 #pragma unroll
@@ -1946,7 +1954,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_coop_kernel(DecodePara
     c.slab = gi % nslabs;
     c.wg = gi;
     c.b = c.slab * 128 + c.grp * 32 + (c.lane & 31);
-    c.row_valid = c.b < p.B;
+    c.row_valid = row_ok(p, c.b, c.sgn);
     c.bc = c.row_valid ? c.b : 0;
     const uint64_t nidx = p.noise_idx[c.member];
     const uint32_t Dbytes = 4u * (uint32_t)p.D;

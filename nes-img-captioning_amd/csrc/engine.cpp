@@ -642,6 +642,18 @@ int nicnes_set_fitness_mode(nicnes_handle* h, int32_t mode) {
     return NICNES_OK;
 }
 
+// [D] zeros + one zero slice index: theta itself as a "member" (the sigma = 0 decodes)
+static int ensure_zero_noise(nicnes_handle* h) {
+    if (h->zero_noise) return NICNES_OK;
+    HIPC(h, hipDeviceSynchronize());
+    int rc = dalloc(h, &h->zero_noise, (size_t)h->D);
+    if (!rc) rc = dalloc(h, &h->zero_idx, 1);
+    if (rc) return rc;
+    HIPC(h, hipMemset(h->zero_noise, 0, (size_t)h->D * sizeof(float)));
+    HIPC(h, hipMemset(h->zero_idx, 0, sizeof(uint64_t)));
+    return NICNES_OK;
+}
+
 int nicnes_evaluate(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
                     double* fitness_out, int32_t* seq_out, void* stream) {
     return nicnes_evaluate_lp(h, iteration, member_begin, count, sigma, fitness_out, seq_out, nullptr, stream);
@@ -653,9 +665,12 @@ int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begi
                                    stream);
 }
 
-int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
-                            const int32_t* member_batch_host, double* fitness_out, int32_t* seq_out, float* logprob_out,
-                            void* stream) {
+// eval_theta: the sigma = 0 rollout of theta itself (count 1), decoded ONCE: sign + takes the first half of the
+// batch's images and sign - the second (at sigma = 0 both signs are theta, so the halves are one decode of the
+// batch), scored as one rollout of B rows
+static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
+                         const int32_t* member_batch_host, double* fitness_out, int32_t* seq_out, float* logprob_out,
+                         void* stream, bool eval_theta) {
     if (!h || !fitness_out || member_begin < 0) return NICNES_ERR_INVALID;
     if (count < 1 || count > h->cfg.max_members) return fail(h, NICNES_ERR_INVALID, "count out of [1, max_members]");
     if (!h->noise) return fail(h, NICNES_ERR_INVALID, "nicnes_set_noise_table first");
@@ -680,13 +695,21 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     } else if (h->n_batches != 1) {
         return fail(h, NICNES_ERR_INVALID, "several batches are held: pass member_batch (nicnes_evaluate_batches)");
     }
-    HIPC(h, nicnes_launch_noise_index(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, h->cfg.noise_len,
-                                      (uint64_t)h->D, h->nidx, s));
     DecodeParams p;
     p.theta = h->theta32;
     p.noise = h->noise;
     p.noise_idx = h->nidx;
-    if (h->mut_mode && !h->dbuf) {   // first mutated evaluation: [max_members, Dp] delta' rows
+    if (eval_theta) {       // theta itself: a zero slice (the sigma-scaled table is left as it is)
+        int rc = ensure_zero_noise(h);
+        if (rc) return rc;
+        p.noise = h->zero_noise;
+        p.noise_idx = h->zero_idx;
+    } else {
+        HIPC(h, nicnes_launch_noise_index(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, h->cfg.noise_len,
+                                          (uint64_t)h->D, h->nidx, s));
+    }
+    if (eval_theta) {
+    } else if (h->mut_mode && !h->dbuf) {   // first mutated evaluation: [max_members, Dp] delta' rows
         HIPC(h, hipDeviceSynchronize());
         h->Dp = (h->D + 63) / 64 * 64;
         int rc = dalloc(h, &h->dbuf, (size_t)h->cfg.max_members * (size_t)h->Dp);
@@ -694,7 +717,8 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
         if (rc) return rc;
         HIPC(h, nicnes_launch_iota_stride(h->didx, h->cfg.max_members, (uint64_t)h->Dp, s));
     }
-    if (h->mut_mode) {      // safe / proportional mutations: the decode reads the members' delta' rows
+    if (eval_theta) {
+    } else if (h->mut_mode) {      // safe / proportional mutations: the decode reads the members' delta' rows
         HIPC(h, nicnes_launch_mutate(h->noise, h->nidx, count, h->D, sigma, h->mut_vec, h->mut_mode, h->dbuf, h->Dp, s));
         p.noise = h->dbuf;
         p.noise_idx = h->didx;
@@ -731,8 +755,10 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     bool bounded = h->bounded_mode == 1 || (h->bounded_mode == 2 && h->exact_left == 0);
     if (h->bounded_mode == 2 && h->exact_left > 0 && !p.lp) --h->exact_left;
     p.bounded_lse = bounded ? 1 : 0;
+    // rows per sign: the batch, or its first half (eval_theta; sign - takes images half + b)
+    const int rows = eval_theta ? (h->B + 1) / 2 : h->B;
     int G = 0, nslabs = 0, S = 0;
-    decode_shape(h, h->B, count, &G, &nslabs, &S);
+    decode_shape(h, rows, count, &G, &nslabs, &S);
     if ((int64_t)count * nslabs * S > h->part_cap)
         return fail(h, NICNES_ERR_INVALID, "decode split beyond the partial-state buffer (nicnes_set_decode_split)");
     p.G = G;
@@ -746,7 +772,9 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     p.coop_ctr = h->coop_ctr;
     p.alive2 = h->alive + h->alive_stride;
     p.alive_stride = h->alive_stride;
-    p.B = h->B;
+    p.B = rows;
+    p.B_img = h->B;
+    p.sign_off = eval_theta ? rows : 0;
     p.F = h->cfg.fc_feat_size;
     p.V1 = h->V1;
     p.T = h->cfg.seq_length;
@@ -761,8 +789,8 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     p.off_h2h_w = h->off[7];
     p.off_h2h_b = h->off[8];
     // rows a member never writes (all finished early) must read as 0 (nets.py:188 zeros)
-    HIPC(h, hipMemsetAsync(p.seq, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(int32_t), s));
-    if (p.lp) HIPC(h, hipMemsetAsync(p.lp, 0, (size_t)count * 2 * h->B * h->cfg.seq_length * sizeof(float), s));
+    HIPC(h, hipMemsetAsync(p.seq, 0, (size_t)count * 2 * rows * h->cfg.seq_length * sizeof(int32_t), s));
+    if (p.lp) HIPC(h, hipMemsetAsync(p.lp, 0, (size_t)count * 2 * rows * h->cfg.seq_length * sizeof(float), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
     int n_ev = 0;
     // the coop launch needs all its workgroups resident: never split over streams
@@ -794,8 +822,9 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
     }
     h->n_dev = h->timing ? n_ev : 0;
     h->multi_stream = nstr > 1;
-    if (p.no_exit)
-        HIPC(h, nicnes_launch_lp_batch_exit(p.seq, p.lp, 2 * count, h->B, h->cfg.seq_length, s));
+    if (p.no_exit)      // eval_theta: the two halves are one rollout
+        HIPC(h, nicnes_launch_lp_batch_exit(p.seq, p.lp, eval_theta ? 1 : 2 * count, eval_theta ? 2 * rows : h->B,
+                                            h->cfg.seq_length, s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     if (!h->stats_pending) {          // read the fallback counter back without a host wait
         HIPC(h, hipMemcpyAsync(h->stats_host, h->stats, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -804,14 +833,31 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
         h->last_bounded = bounded && !p.lp;
     }
     CiderTables tb = tables_of(h);
+    const int n_cand = eval_theta ? 1 : 2 * count;      // eval_theta: rows s * half + b = image s * half + b
     if (h->img_tables)
-        HIPC(h, nicnes_launch_cider_img(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
+        HIPC(h, nicnes_launch_cider_img(p.seq, n_cand, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
                                          h->fitness_mode, h->row_scores, fitness_out, s));
     else
-        HIPC(h, nicnes_launch_cider(p.seq, 2 * count, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
+        HIPC(h, nicnes_launch_cider(p.seq, n_cand, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
                                     h->fitness_mode, fitness_out, s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[2], s));
     return NICNES_OK;
+}
+
+int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
+                            const int32_t* member_batch_host, double* fitness_out, int32_t* seq_out, float* logprob_out,
+                            void* stream) {
+    return evaluate_impl(h, iteration, member_begin, count, sigma, member_batch_host, fitness_out, seq_out, logprob_out,
+                         stream, false);
+}
+
+int nicnes_evaluate_theta(nicnes_handle* h, int32_t batch, double* fitness_out, int32_t* seq_out, float* logprob_out,
+                          void* stream) {
+    if (!h) return NICNES_ERR_INVALID;
+    if (batch < 0 || (h->batch_set && batch >= h->n_batches)) return fail(h, NICNES_ERR_INVALID, "batch outside [0, n_batches)");
+    const int32_t mb = batch;
+    return evaluate_impl(h, 0, 0, 1, 0.f, h->n_batches > 1 ? &mb : nullptr, fitness_out, seq_out, logprob_out, stream,
+                         true);
 }
 
 int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, float* out, void* stream) {
@@ -822,14 +868,14 @@ int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, floa
     hipStream_t s = (hipStream_t)stream;
     HIPC(h, hipSetDevice(h->device));
     const int L = 5, split = 100;                                  // forward_for_sensitivity defaults (nets.py:22)
-    if (!h->zero_noise) {
-        HIPC(h, hipDeviceSynchronize());
-        int rc = dalloc(h, &h->zero_noise, (size_t)h->D);
-        if (!rc) rc = dalloc(h, &h->zero_idx, 1);
-        if (!rc) rc = dalloc(h, &h->sens_tok, (size_t)2 * h->cfg.max_batch * (L - 1));
+    {
+        int rc = ensure_zero_noise(h);
         if (rc) return rc;
-        HIPC(h, hipMemset(h->zero_noise, 0, (size_t)h->D * sizeof(float)));
-        HIPC(h, hipMemset(h->zero_idx, 0, sizeof(uint64_t)));
+    }
+    if (!h->sens_tok) {
+        HIPC(h, hipDeviceSynchronize());
+        int rc = dalloc(h, &h->sens_tok, (size_t)2 * h->cfg.max_batch * (L - 1));
+        if (rc) return rc;
         h->sens = nicnes_sens_create();
     }
     // the greedy tokens of logit steps 1..L-1 from the engine's bit-exact decode of theta itself (sigma 0),
@@ -856,6 +902,8 @@ int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, floa
     p.no_exit = 1;
     p.no_mask = 1;
     p.B = rows;
+    p.B_img = h->B;
+    p.sign_off = 0;
     p.F = h->cfg.fc_feat_size;
     p.V1 = h->V1;
     p.T = L - 1;

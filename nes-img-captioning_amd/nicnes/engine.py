@@ -231,6 +231,20 @@ class Engine:
         out = (fit,) + ((seq,) if return_seq else ()) + ((lp,) if return_lp else ())
         return out if len(out) > 1 else fit
 
+    def evaluate_theta(self, batch=0, return_seq=False, return_lp=False):
+        """Fitness of theta itself on the batch held (or batch `batch` of set_batches'): the sigma = 0
+        rollout (CaptPolicy.rollout) decoded once, sign + over the first half of the images and sign -
+        over the rest. Tensor [1] fp64 on the GPU; return_seq / return_lp add [B, T] tokens / log-probs."""
+        fit = torch.empty(1, dtype=torch.float64, device=self.device)
+        shape = (self.B, self.cfg.seq_length)
+        seq = torch.empty(shape, dtype=torch.int32, device=self.device) if return_seq else None
+        lp = torch.empty(shape, dtype=torch.float32, device=self.device) if return_lp else None
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_evaluate_theta(self.h, int(batch), _ptr(fit), _ptr(seq), _ptr(lp), self._stream()),
+                  self.h, 'evaluate_theta')
+        out = (fit,) + ((seq,) if return_seq else ()) + ((lp,) if return_lp else ())
+        return out if len(out) > 1 else fit
+
     def rank_weights(self, fitness_all):
         """fitness [P, 2] fp64 (whole population) -> (centred ranks [P, 2] fp64, weights [P] fp32)."""
         P = fitness_all.shape[0]

@@ -155,8 +155,10 @@ class EnginePolicy:
         """CaptPolicy.rollout (policies.py:86-128) of the current theta: float(100 * mean CIDEr-D) for
         'greedy', the criterion value for the greedy_* fitness modes."""
         self._ensure_batch(data)
-        fit = self.e.evaluate(0, 0, 1, 0.0, member_batch=member_batches(data, 0, 1))
-        return float(fit[0, 0].item())
+        # theta itself, decoded once (nicnes_evaluate_theta: the two antithetic signs split the images);
+        # with several batches held, member 0's batch (member_batches' rule)
+        fit = self.e.evaluate_theta(0)
+        return float(fit[0].item())
 
 
 # ---------------------------------------------------------------- worker --------------------------

@@ -233,6 +233,108 @@ void run_split(const char* name, const float* w, const float* z, float* out) {
            flops / best / 1e9 / 157.3 * 100.0 / 1000.0, best * 1e3 / nst);
 }
 
+// LDS-DMA staging (glds): W0 and z tiles go global -> LDS with no VGPR destination (8 x 1 KiB
+// global_load_lds_dwordx4 per wave and stage); each wave forms its own sign's A operand at read time
+// (w + z or w - z, VALU per A value). LDS image per plane: 32 "pair rows" of 1 KiB + 16 B pad, pair
+// row p holding matrix rows r0(p) and r0(p) + 16 (r0 = (p & 15) + 32 (p >> 4)): one wave-instruction
+// fills one pair row, and a ds_read_b128 lane group (16 distinct rows r & 15) is conflict-free.
+#define PAIR_BYTES 1040
+#define PLANE_BYTES (32 * PAIR_BYTES)
+#define GBUF_BYTES (2 * PLANE_BYTES)
+typedef __attribute__((address_space(3))) void lds_void;
+template <int MODE, bool NEG>
+__device__ __forceinline__ void glds_stage(const char* buf, int abase, const float (&hB)[64], f32x16& acc0, f32x16& acc1) {
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+        f32x4 a0[4], a1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int off = abase + 16 * (8 * T + c);
+            const f32x4 w0 = *reinterpret_cast<const f32x4*>(buf + off);
+            const f32x4 w1 = *reinterpret_cast<const f32x4*>(buf + off + 16 * PAIR_BYTES);
+            if (MODE == 1) { a0[c] = w0; a1[c] = w1; continue; }
+            const f32x4 z0 = *reinterpret_cast<const f32x4*>(buf + PLANE_BYTES + off);
+            const f32x4 z1 = *reinterpret_cast<const f32x4*>(buf + PLANE_BYTES + off + 16 * PAIR_BYTES);
+            a0[c] = NEG ? w0 - z0 : w0 + z0;
+            a1[c] = NEG ? w1 - z1 : w1 + z1;
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], hB[16 * T + jj], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], hB[16 * T + jj], acc1, 0, 0, 0);
+        }
+    }
+}
+
+template <int MODE, bool NEG>
+__device__ __forceinline__ void glds_loop(char* lds, const float* w, const float* z, int nst, const float (&hB)[64],
+                                          f32x16& acc0, f32x16& acc1) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // this lane's A-operand base: row r = lane & 31 of chain a (chain b: + 16 pair rows), k chunk 4 (lane >> 5)
+    const int r = lane & 31;
+    const int abase = (r & 15) * PAIR_BYTES + (r >> 4) * 512 + 64 * (lane >> 5);
+    // glds: wave w fills pair rows 8w .. 8w + 7 of the planes (waves 0-3: W0, 4-7: z)
+    const float* src = (wave < 4) ? w : z;
+    const size_t gl = (size_t)blockIdx.x * 65536 + (size_t)(16 * (lane >> 5)) * 128 + 4 * (lane & 31);
+    for (int s = 0; s < nst; ++s) {
+        if (s + 1 < nst || MODE == 2) {
+            char* nb = lds + ((s + 1) & 1) * GBUF_BYTES + (wave >> 2) * PLANE_BYTES;
+            const size_t so = gl + (size_t)((s + 1) & 15) * 8192;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int p = 8 * (wave & 3) + j, r0 = (p & 15) + 32 * (p >> 4);
+                __builtin_amdgcn_global_load_lds((const void*)(src + so + (size_t)r0 * 128),
+                                                 (lds_void*)(nb + p * PAIR_BYTES), 16, 0, 0);
+            }
+        }
+        glds_stage<MODE, NEG>(lds + (s & 1) * GBUF_BYTES, abase, hB, acc0, acc1);
+        __syncthreads();
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512) void stage_probe_glds(const float* __restrict__ w, const float* __restrict__ z,
+                                                        float* out, int nst) {
+    extern __shared__ __attribute__((aligned(16))) char glds_buf[];
+    const int tid = threadIdx.x, lane = tid & 63, sgn = tid >> 8;
+    float hB[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) hB[i] = 1e-3f * (float)((lane + i) & 7);
+    for (int i = tid; i < 2 * GBUF_BYTES / 4; i += 512) reinterpret_cast<float*>(glds_buf)[i] = 1e-3f * (float)(i & 15);
+    __syncthreads();
+    f32x16 acc0 = {}, acc1 = {};
+    if (sgn) glds_loop<MODE, true>(glds_buf, w, z, nst, hB, acc0, acc1);
+    else glds_loop<MODE, false>(glds_buf, w, z, nst, hB, acc0, acc1);
+    float r = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r += acc0[i] + acc1[i];
+    out[blockIdx.x * 512 + tid] = r;
+}
+
+template <int MODE>
+void run_glds(const char* name, const float* w, const float* z, float* out) {
+    const int nst = 150, blocks = 256;
+    const size_t lds = 2 * GBUF_BYTES;
+    hipFuncSetAttribute((const void*)stage_probe_glds<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipLaunchKernelGGL((stage_probe_glds<MODE>), dim3(blocks), dim3(512), lds, 0, w, z, out, 10);
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; ++rep) {
+        hipEventRecord(e0);
+        hipLaunchKernelGGL((stage_probe_glds<MODE>), dim3(blocks), dim3(512), lds, 0, w, z, out, nst);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        best = ms < best ? ms : best;
+    }
+    const double flops = (double)blocks * 8 * nst * 128 * 32 * 32 * 2 * 2;
+    printf("%-40s %8.3f ms  %7.1f TFLOP/s  %5.1f%% of 157.3  %6.2f us/stage\n", name, best, flops / best / 1e9,
+           flops / best / 1e9 / 157.3 * 100.0 / 1000.0, best * 1e3 / nst);
+}
+
 int main() {
     float *w, *z, *out;
     const size_t n = (size_t)256 * 65536 + 16 * 8192 + 8192;
@@ -252,5 +354,8 @@ int main() {
     run<true, true, 6>("W+- staging by the sign-0 waves only", w, z, out);
     run_split("sign-split: 2 x 4-wave workgroups per CU", w, z, out);
     run<true, true, 1>("A from LDS, barrier, W+- staging (again)", w, z, out);
+    run_glds<0>("glds W0+z, W+- formed at A read", w, z, out);
+    run_glds<1>("glds W0+z, A = W0 (no z read, no VALU)", w, z, out);
+    run_glds<0>("glds W0+z, W+- formed at A read (again)", w, z, out);
     return 0;
 }

@@ -100,6 +100,13 @@ class OracleEngine:
                 out[k, s] = CR.criterion_fitness(self.fitness_mode, lp, seq, scores) if self.fitness_mode else f
         return out
 
+    def evaluate_theta(self, batch=0):
+        fc, gts = (self.fc, self.gts) if not getattr(self, 'batches', None) else self.batches[batch]
+        seq, lp, _ = O.decode(self.dims, self.theta32, fc)
+        f, scores = CR.rollout_fitness(self.scorer, seq, gts)
+        return torch.tensor([CR.criterion_fitness(self.fitness_mode, lp, seq, scores) if self.fitness_mode else f],
+                            dtype=torch.float64)
+
     def rank_weights(self, fitness_all):
         w, cr = O.weights_from_fitness(fitness_all.numpy())
         return torch.from_numpy(cr), torch.from_numpy(w)
