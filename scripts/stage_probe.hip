@@ -28,7 +28,8 @@ __global__ __launch_bounds__(512) void stage_probe(const float* __restrict__ w, 
     f32x16 acc0 = {}, acc1 = {};
     f32x4 sw[4], sz[4];
     const size_t so = (size_t)blockIdx.x * 65536 + 4 * tid;
-    if (STAGE == 1 || STAGE == 2 || STAGE == 5) {
+    const size_t zs = (size_t)blockIdx.x * (size_t)(nst + 1) * 8192 + 4 * tid;   // STAGE 7: the block's z stream
+    if (STAGE == 1 || STAGE == 2 || STAGE == 5 || STAGE == 7) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) { sw[u] = *(const f32x4*)(w + so + 2048 * u); sz[u] = *(const f32x4*)(z + so + 2048 * u); }
     } else {
@@ -55,6 +56,11 @@ __global__ __launch_bounds__(512) void stage_probe(const float* __restrict__ w, 
         if (STAGE == 1 || STAGE == 2) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) { nw[u] = *(const f32x4*)(w + o2 + 2048 * u); nz[u] = *(const f32x4*)(z + o2 + 2048 * u); }
+        }
+        if (STAGE == 7) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { nw[u] = *(const f32x4*)(w + o2 + 2048 * u);
+                                          nz[u] = *(const f32x4*)(z + zs + (size_t)(s + 1) * 8192 + 2048 * u); }
         }
 #pragma unroll
         for (int T = 0; T < 4; ++T) {
@@ -95,7 +101,7 @@ __global__ __launch_bounds__(512) void stage_probe(const float* __restrict__ w, 
                 sw[u] = nw[u]; sz[u] = nz[u]; sw2[u] = mw[u]; sz2[u] = mz[u];
             }
         }
-        if (STAGE == 1 || STAGE == 5) {
+        if (STAGE == 1 || STAGE == 5 || STAGE == 7) {
             float* b = lds + ((s + 1) & 1) * STAGE_FLOATS + (tid >> 5) * LDS_ROW + 4 * (tid & 31);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -253,6 +259,11 @@ __device__ __forceinline__ void glds_stage(const char* buf, int abase, const flo
             const f32x4 w0 = *reinterpret_cast<const f32x4*>(buf + off);
             const f32x4 w1 = *reinterpret_cast<const f32x4*>(buf + off + 16 * PAIR_BYTES);
             if (MODE == 1) { a0[c] = w0; a1[c] = w1; continue; }
+            if (MODE >= 3) {              // pre-formed W+- planes: the sign's own plane, no VALU
+                a0[c] = *reinterpret_cast<const f32x4*>(buf + (NEG ? PLANE_BYTES : 0) + off);
+                a1[c] = *reinterpret_cast<const f32x4*>(buf + (NEG ? PLANE_BYTES : 0) + off + 16 * PAIR_BYTES);
+                continue;
+            }
             const f32x4 z0 = *reinterpret_cast<const f32x4*>(buf + PLANE_BYTES + off);
             const f32x4 z1 = *reinterpret_cast<const f32x4*>(buf + PLANE_BYTES + off + 16 * PAIR_BYTES);
             a0[c] = NEG ? w0 - z0 : w0 + z0;
@@ -279,12 +290,35 @@ __device__ __forceinline__ void glds_loop(char* lds, const float* w, const float
     for (int s = 0; s < nst; ++s) {
         if (s + 1 < nst || MODE == 2) {
             char* nb = lds + ((s + 1) & 1) * GBUF_BYTES + (wave >> 2) * PLANE_BYTES;
+            if (MODE == 5) {              // as MODE 3 through a buffer resource (buffer_load ... lds, soffset per row)
+                const size_t cyc = (size_t)nst + 1;
+                const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+                    (void*)(w + (size_t)blockIdx.x * cyc * 16384), (short)0, (int)(cyc * 16384 * 4), 0x00020000);
+                const unsigned soff = 4u * (unsigned)(((s + 1) % cyc) * 16384 + (wave >> 2) * 8192);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int p = 8 * (wave & 3) + j;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, (lds_void*)(nb + p * PAIR_BYTES), 16, 16 * lane,
+                                                             (int)(soff + 1024u * p), 0, 0);
+                }
+            } else if (MODE >= 3) {              // pre-formed image: 1 KiB per pair row, the workgroup's own stream
+                const size_t cyc = MODE == 3 ? (size_t)nst + 1 : 16;
+                const size_t so = (size_t)blockIdx.x * cyc * 16384 + (size_t)((s + 1) % cyc) * 16384 +
+                                  (size_t)(wave >> 2) * 8192 + 4 * lane;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int p = 8 * (wave & 3) + j;
+                    __builtin_amdgcn_global_load_lds((const void*)(w + so + 256 * p),
+                                                     (lds_void*)(nb + p * PAIR_BYTES), 16, 0, 0);
+                }
+            } else {
             const size_t so = gl + (size_t)((s + 1) & 15) * 8192;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int p = 8 * (wave & 3) + j, r0 = (p & 15) + 32 * (p >> 4);
                 __builtin_amdgcn_global_load_lds((const void*)(src + so + (size_t)r0 * 128),
                                                  (lds_void*)(nb + p * PAIR_BYTES), 16, 0, 0);
+            }
             }
         }
         glds_stage<MODE, NEG>(lds + (s & 1) * GBUF_BYTES, abase, hB, acc0, acc1);
@@ -354,8 +388,18 @@ int main() {
     run<true, true, 6>("W+- staging by the sign-0 waves only", w, z, out);
     run_split("sign-split: 2 x 4-wave workgroups per CU", w, z, out);
     run<true, true, 1>("A from LDS, barrier, W+- staging (again)", w, z, out);
-    run_glds<0>("glds W0+z, W+- formed at A read", w, z, out);
     run_glds<1>("glds W0+z, A = W0 (no z read, no VALU)", w, z, out);
-    run_glds<0>("glds W0+z, W+- formed at A read (again)", w, z, out);
+    float* big;
+    const size_t nbig = (size_t)256 * 151 * 16384;
+    hipMalloc(&big, nbig * sizeof(float));
+    hipMemset(big, 0, nbig * sizeof(float));
+    run<true, true, 7>("reg staging, z streamed from HBM", w, big, out);
+    run_glds<3>("glds pre-formed W+- from HBM", big, z, out);
+    run_glds<4>("glds pre-formed W+- (L2-resident)", big, z, out);
+    run<true, true, 7>("reg staging, z streamed from HBM (again)", w, big, out);
+    run_glds<3>("glds pre-formed W+- from HBM (again)", big, z, out);
+    run_glds<5>("buffer_load lds pre-formed W+- from HBM", big, z, out);
+    run_glds<5>("buffer_load lds pre-formed W+- (again)", big, z, out);
+    run<true, true, 0>("A from LDS, barrier per stage (again)", w, z, out);
     return 0;
 }
