@@ -125,13 +125,14 @@ def rollout_fitness(scorer, seq, gts_rows, seq_per_img=1):
 
 # greedy_* fitness criteria (pinned by tests/golden/fitness_criteria.npz, made from the reference's own
 # classes by scripts/make_golden.py). Codes match nicnes_set_fitness_mode.
-CRITERIA = {'greedy': 0, 'greedy_logprob': 1, 'greedy_expprob': 2, 'greedy_linprob': 3, 'greedy_avgprob': 4}
+CRITERIA = {'greedy': 0, 'greedy_logprob': 1, 'greedy_expprob': 2, 'greedy_linprob': 3, 'greedy_avgprob': 4,
+            'sample': 5, 'self_critical': 6, 'sc_loss': 7}
 
 
 def criterion_fitness(mode, lp, seq, scores):
     """``crit(sample_logprobs, gen_result, rewards)`` of CaptPolicy.rollout (policies.py:119-123) for
     the criteria Fitness.get_criterium picks (policies.py:50-61): AltLog (fitness.py:43-64), Exp
-    (:90-109), Lin (:112-132), AvgLog (:67-86). Elementwise in fp32 like torch; the sums in fp64.
+    (:90-109), Lin (:112-132), AvgLog (:67-86), and Log (:12-40) for sc_loss. Elementwise in fp32 like torch; the sums in fp64.
     ``lp`` f32 [N, T] per-step log-prob of the chosen token, ``seq`` [N, T], ``scores`` [N] CIDEr-D
     per row (rewards = scores repeated over T, policies.py:191; cast to fp32 at policies.py:121)."""
     code = CRITERIA[mode] if isinstance(mode, str) else int(mode)
@@ -149,6 +150,8 @@ def criterion_fitness(mode, lp, seq, scores):
         out = p * reward * mask
     elif code == 4:
         out = np.float32(0.5) * reward * mask + np.float32(0.5) * pfact * reward * mask
+    elif code == 7:                     # sc_loss: LogFitnessCriterion (fitness.py:12-40), rewards = sample - greedy
+        out = -lp * reward * mask
     else:
         raise ValueError('criterion %r' % (mode,))
     return float(out.astype(np.float64).sum() / mask.astype(np.float64).sum())

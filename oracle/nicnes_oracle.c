@@ -6,7 +6,7 @@
  * and bench.py's cpu_baseline leg.
  *
  * Restates (op for op, one row at a time):
- *   FCModel._sample        /root/reference/src/captioning/nets.py:183-245
+ *   FCModel._sample        /root/reference/src/captioning/nets.py:183-245 (greedy and sampled)
  *   LSTMCore.forward       /root/reference/src/captioning/nets.py:98-134   (vbn = layer_n = false)
  *   F.log_softmax + torch.max (first index on ties)   nets.py:202,208-209
  * Dense products are fp32 fma chains started from the bias in the order nn_kperm()
@@ -131,6 +131,35 @@ static int greedy_pick(const float* logits, int V1, float* lp_out, uint8_t* frag
     return tok;
 }
 
+/* sampled pick (nets.py:210-231, greedy=False): p = exp(log_softmax) in fp32 (torch.exp), n = p /
+ * sum(p) in fp32 (np.linalg.norm(row, ord=1)), then RandomState.choice(len, 1, p=n): cdf = cumsum(n)
+ * in fp64 divided by its last entry, pick = first index with cdf > u (searchsorted side='right').
+ * lp = the pick's log-prob (logprobs.gather). fragile = u within 1e-6 of the cdf boundary below or at
+ * the pick (a different summation order of p moves the boundaries by ~1e-7). pbuf/cdf: [V1] scratch. */
+static int sample_pick(const float* logits, int V1, double u, float* pbuf, double* cdf, float* lp_out,
+                       uint8_t* fragile) {
+    float m = logits[0];
+    for (int v = 1; v < V1; ++v) if (logits[v] > m) m = logits[v];
+    double s = 0.0;
+    for (int v = 0; v < V1; ++v) s += exp((double)(logits[v] - m));
+    const float lse = (float)log(s);
+    double norm = 0.0;
+    for (int v = 0; v < V1; ++v) { pbuf[v] = nn_expf((logits[v] - m) - lse); norm += pbuf[v]; }
+    const float normf = (float)norm;
+    double c = 0.0;
+    for (int v = 0; v < V1; ++v) { c += (double)(pbuf[v] / normf); cdf[v] = c; }
+    const double last = cdf[V1 - 1];
+    int tok = V1 - 1;
+    for (int v = 0; v < V1; ++v) if (cdf[v] / last > u) { tok = v; break; }
+    const double hi = cdf[tok] / last, lo = tok > 0 ? cdf[tok - 1] / last : 0.0;
+    *fragile = (fabs(hi - u) < 1e-6 || fabs(u - lo) < 1e-6) ? 1 : 0;
+    *lp_out = (logits[tok] - m) - lse;
+    return tok;
+}
+
+static int decode_core(const od_dims* d, const float* theta, const float* fc, int B, const double* u,
+                       int32_t* seq, float* lp, uint8_t* fragile, int half_order);
+
 /*
  * Greedy decode of B unique rows with a (possibly perturbed) fp32 theta.
  * seq[B*T] (int32), lp[B*T] (max log-prob per step; 0 after the global early exit, as
@@ -138,6 +167,22 @@ static int greedy_pick(const float* logits, int V1, float* lp_out, uint8_t* frag
  */
 int od_decode(const od_dims* d, const float* theta, const float* fc, int B,
               int32_t* seq, float* lp, uint8_t* fragile, int half_order) {
+    return decode_core(d, theta, fc, B, NULL, seq, lp, fragile, half_order);
+}
+
+/*
+ * Sampled decode (FCModel._sample with greedy=False, nets.py:210-243): row b draws u[b*T + t-1] at logit
+ * step t, every row at every step until the whole batch has finished, as the reference draws one uniform
+ * per row and step (np.random.choice per row, nets.py:220-224). lp = log-prob of the sampled token (also
+ * for rows already finished, as seq_logprobs keeps it), 0 after the global early exit.
+ */
+int od_decode_sample(const od_dims* d, const float* theta, const float* fc, int B, const double* u,
+                     int32_t* seq, float* lp, uint8_t* fragile, int half_order) {
+    return decode_core(d, theta, fc, B, u, seq, lp, fragile, half_order);
+}
+
+static int decode_core(const od_dims* d, const float* theta, const float* fc, int B, const double* u,
+                       int32_t* seq, float* lp, uint8_t* fragile, int half_order) {
     const od_layout L = od_make_layout(d);
     const int E = d->E, R = d->R, F = d->F, V1 = d->V1, T = d->T, G = 5 * R;
     float* WimgT = transpose_perm(theta + L.img_w, E, F, half_order);
@@ -157,6 +202,8 @@ int od_decode(const od_dims* d, const float* theta, const float* fc, int B,
         float* si = (float*)malloc(sizeof(float) * (size_t)G);
         float* sh = (float*)malloc(sizeof(float) * (size_t)G);
         float* logits = (float*)malloc(sizeof(float) * (size_t)V1);
+        float* pbuf = u ? (float*)malloc(sizeof(float) * (size_t)V1) : NULL;
+        double* cdf = u ? (double*)malloc(sizeof(double) * (size_t)V1) : NULL;
         int unfinished = 1, it = 0;
         fin_step[b] = T;
         for (int t = 0; t <= T; ++t) {
@@ -178,7 +225,8 @@ int od_decode(const od_dims* d, const float* theta, const float* fc, int B,
             gemv_chain(WlT, theta + L.log_b, h, V1, R, half_order, logits);
             float lpv;
             uint8_t fr;
-            int tok = greedy_pick(logits, V1, &lpv, &fr);
+            int tok = u ? sample_pick(logits, V1, u[(size_t)b * T + t - 1], pbuf, cdf, &lpv, &fr)
+                        : greedy_pick(logits, V1, &lpv, &fr);
             if (tok > 0 && unfinished) unfinished = 1; else unfinished = 0;
             it = tok * unfinished;
             seq[(size_t)b * T + t - 1] = it;
@@ -187,7 +235,7 @@ int od_decode(const od_dims* d, const float* theta, const float* fc, int B,
             if (!unfinished && fin_step[b] == T) fin_step[b] = t;
             if (t == T) break;
         }
-        free(x); free(h); free(c); free(si); free(sh); free(logits);
+        free(x); free(h); free(c); free(si); free(sh); free(logits); free(pbuf); free(cdf);
     }
     /* global early exit (nets.py:242-243): steps after every row finished stay 0 */
     int last = 0;

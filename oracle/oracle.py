@@ -48,6 +48,7 @@ def lib():
             build()
         L = ctypes.CDLL(LIB_PATH)
         L.od_decode.restype = ctypes.c_int
+        L.od_decode_sample.restype = ctypes.c_int
         L.od_param_count.restype = ctypes.c_int64
         _lib = L
     return _lib
@@ -163,6 +164,24 @@ def decode(dims, theta32, fc, half_order=0):
     d = dims.c()
     lib().od_decode(ctypes.byref(d), _p(theta32), _p(fc), ctypes.c_int(B), _p(seq), _p(lp), _p(fr),
                     ctypes.c_int(half_order))
+    return seq, lp, fr
+
+
+def decode_sample(dims, theta32, fc, u, half_order=0):
+    """Sampled decode (FCModel._sample, greedy=False, nets.py:210-231) of B rows with the uniforms
+    u [B, T] fp64 (row b's draw at logit step t in u[b, t-1]). Returns (seq, lp, fragile) as decode;
+    fragile marks a draw within 1e-6 of a cdf boundary at the pick."""
+    theta32 = np.ascontiguousarray(theta32, np.float32)
+    fc = np.ascontiguousarray(fc, np.float32)
+    B = fc.shape[0]
+    u = np.ascontiguousarray(u, np.float64)
+    assert theta32.size == dims.D and fc.shape[1] == dims.F and u.shape == (B, dims.T)
+    seq = np.zeros((B, dims.T), np.int32)
+    lp = np.zeros((B, dims.T), np.float32)
+    fr = np.zeros((B, dims.T), np.uint8)
+    d = dims.c()
+    lib().od_decode_sample(ctypes.byref(d), _p(theta32), _p(fc), ctypes.c_int(B), _p(u), _p(seq), _p(lp), _p(fr),
+                           ctypes.c_int(half_order))
     return seq, lp, fr
 
 

@@ -41,7 +41,11 @@ Fixtures (all .npz, loadable with allow_pickle=False):
                                   for SM-G-SUM with a set sensitivity and for SM-PROPORTIONAL; and the SM-G-SUM
                                   sensitivity itself, Sensitivity.calc_sensitivity (safe_mutations.py:34-117)
                                   on a tiny FCModel through forward_for_sensitivity (captioning/nets.py:22-70)
-  fitness_criteria.npz            the greedy_* fitness criteria (src/captioning/fitness.py:43-132, chosen
+  decode_sample.npz               FCModel._sample(greedy=False) (nets.py:210-231) with the global numpy RNG
+                                  seeded: tokens, seq_logprobs and the uniforms RandomState.choice drew
+                                  (replayed and checked step by step), tiny and full dims
+  fitness_criteria.npz            the greedy_* fitness criteria and sc_loss's LogFitnessCriterion
+                                  (src/captioning/fitness.py:12-132, chosen
                                   by Fitness.get_criterium, src/captioning/policies.py:50-61) on seeded
                                   logprobs / sequences / per-row CIDEr rewards, as CaptPolicy.rollout
                                   calls them (policies.py:119-123)
@@ -176,6 +180,73 @@ def decode_bench_fixture(B=128, name='decode_bench_xavier'):
                         sigma=np.float64(SIGMA), members=members, seq=np.stack(seqs).astype(np.int16),
                         margins=np.stack(mars), logprobs=np.stack(lps), dup_consistent=np.array(dup))
     print(name, 'copies consistent', all(dup), 'min margin', float(np.stack(mars).min()))
+
+
+def ref_sample(model, fc, seed):
+    """FCModel._sample(greedy=False) (nets.py:210-231) with the global numpy RNG seeded, and the uniforms it
+    drew: RandomState.choice(len, 1, p) takes one random_sample() per call, one call per row and step
+    (rows in order) from t = 0 (the image step, whose pick is discarded) until every row has finished. The draws are replayed from the same seed and the decode
+    is re-run step by step with the reference's own modules and that choice rule (cdf = cumsum(p / |p|_1) in
+    fp64 / its last entry, searchsorted side='right'); the replayed tokens are asserted equal, which pins
+    the draw order. Returns seq, seq_logprobs, u [B, T] (0 after the last step drawn) and the distance of
+    each draw from the nearest cdf boundary of its pick (u_margin, inf where not drawn)."""
+    fct = torch.from_numpy(fc)
+    np.random.seed(seed)
+    seq, slp = model._sample(fct, greedy=False)
+    B, T = seq.shape
+    np.random.seed(seed)
+    # the loop samples at t = 0 too (the image step, nets.py:203-224; its pick is replaced by <bos>), so
+    # B draws precede logit step 1's
+    draws = np.random.random_sample(B * (T + 1)).reshape(T + 1, B)[1:]
+    u = np.zeros((B, T), np.float64)
+    margin = np.full((B, T), np.inf)
+    state = model.init_hidden(B)
+    _, state = model.core(model.img_embed(fct), state)
+    it = fct.new_zeros(B, dtype=torch.long)
+    unfinished = None
+    for t in range(1, T + 1):
+        out, state = model.core(model.embed(it), state)
+        lp = torch.nn.functional.log_softmax(model.logit(out), dim=1)
+        prob = torch.exp(lp).numpy()
+        pick = np.zeros(B, np.int64)
+        for b in range(B):
+            n_row = prob[b] / np.linalg.norm(prob[b], ord=1)
+            cdf = n_row.astype(np.float64).cumsum()
+            cdf /= cdf[-1]
+            ub = draws[t - 1, b]
+            k = int(cdf.searchsorted(ub, side='right'))
+            pick[b] = k
+            u[b, t - 1] = ub
+            margin[b, t - 1] = min(abs(cdf[k] - ub), abs(ub - cdf[k - 1]) if k > 0 else np.inf)
+        itn = torch.from_numpy(pick)
+        unfinished = (itn > 0) if t == 1 else unfinished * (itn > 0)
+        it = itn * unfinished.type_as(itn)
+        assert torch.equal(it, seq[:, t - 1]), 'replayed draws diverged from _sample'
+        if unfinished.sum() == 0:
+            break
+    return seq.numpy().astype(np.int32), slp.numpy().astype(np.float32), u, margin
+
+
+def decode_sample_fixture():
+    """decode_sample.npz: FCModel._sample(greedy=False) on tiny dims (stored theta, peaked and flat) and on
+    the full fc_caption dims (xavier and peaked theta from their seeds, 40 rows), with the draws."""
+    out = {}
+    cases = [('tiny_wc', O.Dims(vocab_size=63, E=32, R=32, F=64), 2, 4.0, 0.1, 8, 11),
+             ('tiny_xavier', O.Dims(vocab_size=63, E=32, R=32, F=64), 1, 1.0, 0.0, 8, 12),
+             ('full_xavier', O.Dims(), 0, 1.0, 0.0, 40, 13),
+             ('full_wc', O.Dims(), 0, 4.0, 0.1, 40, 14)]
+    for name, d, tseed, gain, bstd, B, seed in cases:
+        model = ref_model(d)
+        theta = O.make_theta(d, tseed, gain, bstd)
+        load_theta(model, theta)
+        fc = np.random.Generator(np.random.PCG64(1234)).standard_normal((B, d.F)).astype(np.float32)
+        seq, slp, u, mar = ref_sample(model, fc, seed)
+        out.update({name + '_dims': np.array([d.vocab_size, d.E, d.R, d.F, d.T], np.int64),
+                    name + '_theta_seed': np.int64(tseed), name + '_gain': np.float64(gain),
+                    name + '_bias_std': np.float64(bstd), name + '_B': np.int64(B), name + '_seq': seq,
+                    name + '_logprobs': slp, name + '_u': u, name + '_u_margin': mar})
+        print(name, 'seq[0]', seq[0], 'min u margin', float(mar.min()))
+    np.savez_compressed(os.path.join(OUT, 'decode_sample.npz'), **out)
 
 
 def decode_bench_b64_fixture():
@@ -376,7 +447,8 @@ def ranks_fixture():
 def fitness_criteria_fixture():
     import captioning.fitness as ref_fit  # noqa: E402  (reference module)
     crits = {'greedy_logprob': ref_fit.AltLogFitnessCriterion, 'greedy_expprob': ref_fit.ExpFitnessCriterion,
-             'greedy_linprob': ref_fit.LinFitnessCriterion, 'greedy_avgprob': ref_fit.AvgLogFitnessCriterion}
+             'greedy_linprob': ref_fit.LinFitnessCriterion, 'greedy_avgprob': ref_fit.AvgLogFitnessCriterion,
+             'sc_loss': ref_fit.LogFitnessCriterion}
     rng = np.random.Generator(np.random.PCG64(77))
     cases = {}
     for case, (N, T) in enumerate([(8, 16), (40, 16), (5, 16)]):
@@ -389,6 +461,8 @@ def fitness_criteria_fixture():
         scores = rng.uniform(0, 3, N).astype(np.float64)
         if case == 2:
             scores[:] = 0.0
+        if case == 1:                           # self-critical rewards (sample - greedy) take either sign
+            scores -= 1.5
         cases['seq_%d' % case], cases['lp_%d' % case], cases['scores_%d' % case] = seq, lp, scores
         reward = np.repeat(scores[:, None], T, 1)          # compute_ciders, policies.py:191
         for name, cls in crits.items():
@@ -404,6 +478,7 @@ def all_fixtures():
     decode_fixture('decode_tiny_wc', tiny, 2, 4.0, 0.1, 1234, 8, True)
     decode_fixture('decode_full_xavier', full, 0, 1.0, 0.0, 1234, 16, False, members=(0, 1))
     decode_fixture('decode_full_wc', full, 0, 4.0, 0.1, 1234, 16, False, members=(0, 1))
+    decode_sample_fixture()
     perturb_fixture()
     adam_fixture()
     ranks_fixture()

@@ -77,7 +77,7 @@ def test_rollout_fitness_dedup_equals_duplicated():
     assert f_unique == pytest.approx(f_dup, rel=1e-12)
 
 
-@pytest.mark.parametrize('mode', ['greedy_logprob', 'greedy_expprob', 'greedy_linprob', 'greedy_avgprob'])
+@pytest.mark.parametrize('mode', ['greedy_logprob', 'greedy_expprob', 'greedy_linprob', 'greedy_avgprob', 'sc_loss'])
 def test_criterion_oracle_matches_reference_golden(mode):
     """greedy_* criteria (src/captioning/fitness.py:43-132) against the reference's own classes
     (tests/golden/fitness_criteria.npz, scripts/make_golden.py); the reference sums in fp32."""

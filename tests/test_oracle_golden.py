@@ -203,3 +203,38 @@ def test_master_ranks_and_gradient_match_reference(golden_dir):
     assert np.abs(g - z['grad']).max() <= 1e-6 * np.abs(z['grad']).max()
     assert [O.noise_index(int(z['noise_seed']), int(z['iteration']), i, int(z['noise_len']), O.Dims().D)
             for i in (0, 511)] == [int(idx[0]), int(idx[511])]
+
+
+SAMPLE_CASES = ['tiny_wc', 'tiny_xavier', 'full_xavier', 'full_wc']
+U_MARGIN = 1e-6   # a draw this close to a cdf boundary of its pick depends on the order p is summed in
+
+
+def sample_case(golden_dir, name):
+    """(dims, theta, fc, golden dict) of one decode_sample.npz case (scripts/make_golden.py)."""
+    z = np.load('%s/decode_sample.npz' % golden_dir)
+    g = {k[len(name) + 1:]: z[k] for k in z.files if k.startswith(name + '_')}
+    V, E, R, F, T = (int(v) for v in g['dims'])
+    d = O.Dims(V, E, R, F, T)
+    theta = O.make_theta(d, int(g['theta_seed']), float(g['gain']), float(g['bias_std']))
+    fc = np.random.Generator(np.random.PCG64(1234)).standard_normal((int(g['B']), d.F)).astype(np.float32)
+    return d, theta, fc, g
+
+
+@pytest.mark.parametrize('name', SAMPLE_CASES)
+def test_sampled_decode_matches_reference(golden_dir, name):
+    """FCModel._sample(greedy=False) (nets.py:210-231) with the uniforms the reference drew: the oracle's
+    tokens equal the reference's on every row up to its first draw within U_MARGIN of a cdf boundary,
+    and the sampled token's log-prob (seq_logprobs) to 5e-6 there."""
+    d, theta, fc, g = sample_case(golden_dir, name)
+    seq, lp, fr = O.decode_sample(d, theta, fc, g['u'])
+    compared = 0
+    for b in range(seq.shape[0]):
+        for t in range(d.T):
+            if g['u_margin'][b, t] < U_MARGIN or fr[b, t]:
+                break
+            assert seq[b, t] == g['seq'][b, t], (name, b, t, seq[b], g['seq'][b])
+            assert abs(lp[b, t] - g['logprobs'][b, t]) <= 5e-6 * max(1.0, abs(g['logprobs'][b, t])), (b, t)
+            compared += 1
+    assert compared >= 0.8 * seq.size, compared
+    if name.startswith('tiny'):
+        assert np.array_equal(seq, g['seq'])
