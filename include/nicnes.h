@@ -122,14 +122,29 @@ int nicnes_set_mutation(nicnes_handle* h, int32_t mode, const float* vec, void* 
 
 /* Fitness criterion (Fitness enum + get_criterium, src/captioning/policies.py:22-61, applied at
  * :119-125): GREEDY = 100 * mean CIDEr-D; the greedy_* modes weight each step's probability of the
- * greedy token by the row's CIDEr-D (src/captioning/fitness.py:43-132). Other modes (sample,
- * self_critical, sc_loss) return NICNES_ERR_UNSUPPORTED. */
+ * greedy token by the row's CIDEr-D (src/captioning/fitness.py:43-132). The sampled modes decode with
+ * FCModel._sample(greedy=False) (src/captioning/nets.py:210-231: each row draws its token from the
+ * softmax with one uniform per row and step) on the fused path: SAMPLE = 100 * mean CIDEr-D of the
+ * sampled rows; SELF_CRITICAL = 100 * mean of (sampled row's score - greedy row's score), the greedy
+ * decode of the same member run first (compute_ciders, policies.py:145-193); SC_LOSS =
+ * LogFitnessCriterion (fitness.py:12-40) of the sampled log-probs with those differences as rewards.
+ * Sampled rows are not deduplicated: pass the batch with its seq_per_img copies per image (the rows
+ * the reference samples independently). */
 #define NICNES_FITNESS_GREEDY 0
 #define NICNES_FITNESS_GREEDY_LOGPROB 1   /* AltLogFitnessCriterion */
 #define NICNES_FITNESS_GREEDY_EXPPROB 2   /* ExpFitnessCriterion */
 #define NICNES_FITNESS_GREEDY_LINPROB 3   /* LinFitnessCriterion */
 #define NICNES_FITNESS_GREEDY_AVGPROB 4   /* AvgLogFitnessCriterion */
+#define NICNES_FITNESS_SAMPLE 5           /* 'sample' */
+#define NICNES_FITNESS_SELF_CRITICAL 6    /* 'self_critical' */
+#define NICNES_FITNESS_SC_LOSS 7          /* 'sc_loss': LogFitnessCriterion */
 int nicnes_set_fitness_mode(nicnes_handle* h, int32_t mode);
+
+/* Draws of the sampled modes (not a reference interface; the test hook that replays the reference's
+ * numpy draws): the uniforms the next sampled evaluates use, u_host [count, 2, B, seq_length] fp64 (member,
+ * sign, row, logit step), copied; n = 0 returns to the engine's own draws (a counter-based hash of the
+ * noise seed, iteration, member, sign, row and step, 53-bit like RandomState.random_sample). */
+int nicnes_set_sample_draws(nicnes_handle* h, const double* u_host, int64_t n);
 
 /* nicnes_evaluate plus the per-step log-prob of each greedy token, FCModel._sample's seq_logprobs
  * (src/captioning/nets.py:191,208,241): logprob_out [count, 2, B, seq_length] fp32 or NULL. */

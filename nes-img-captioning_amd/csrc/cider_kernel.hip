@@ -151,12 +151,16 @@ __global__ __launch_bounds__(256) void nicnes_cook_refs_kernel(const int32_t* re
 // per-step log-probs, rewards = per-row score as fp32 (policies.py:121,191), mask = 1 at t = 0 then
 // seq[t-1] > 0; elementwise in fp32 as torch does, sum(out) / sum(mask) accumulated in fp64
 // (fitness.py:43-132).
+// crit 5 ('sample'): as 'greedy' over the sampled rows. crit 6 ('self_critical', compute_ciders,
+// policies.py:174-184): 100 * mean of (sample score - greedy score) per row, base = the greedy rows'
+// scores. crit 7 ('sc_loss'): LogFitnessCriterion (fitness.py:12-40), -lp * reward * mask with reward =
+// the row's self-critical score difference (policies.py:119-123, get_criterium :50-52).
 __device__ void finish_fitness(const double* row_score, const int32_t* seq, const float* lp, int B, int T, int crit,
-                               double* out) {
-    if (crit == 0 || lp == nullptr) {
+                               double* out, const double* base = nullptr) {
+    if (crit == 0 || crit == 5 || crit == 6 || lp == nullptr) {
         if (threadIdx.x == 0) {
             double s = 0.0;
-            for (int b = 0; b < B; ++b) s += row_score[b];
+            for (int b = 0; b < B; ++b) s += row_score[b] - (crit == 6 && base ? base[b] : 0.0);
             *out = (s / (double)B) * 100.0;
         }
         return;
@@ -165,12 +169,14 @@ __device__ void finish_fitness(const double* row_score, const int32_t* seq, cons
     double num = 0.0, den = 0.0;
     const float third = (float)(1.0 / 9.0), l9 = (float)0.9542425094393249, em1 = (float)(2.718281828459045 - 1.0);
     for (int b = threadIdx.x; b < B; b += blockDim.x) {
-        const float reward = (float)row_score[b];
+        const float reward = (float)(row_score[b] - (base ? base[b] : 0.0));
         for (int t = 0; t < T; ++t) {
             if (t > 0 && seq[(size_t)b * T + t - 1] <= 0) break;   // masked from here on
             const float p = expf(lp[(size_t)b * T + t]);
             float o;
-            if (crit == 2) {
+            if (crit == 7) {
+                o = -lp[(size_t)b * T + t] * reward;
+            } else if (crit == 2) {
                 o = (expf(p) - 1.0f) / em1 * reward;
             } else if (crit == 3) {
                 o = p * reward;
@@ -195,7 +201,8 @@ __device__ void finish_fitness(const double* row_score, const int32_t* seq, cons
 // ---- candidates: one workgroup per candidate, one wave per image row ---------------------------
 __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, int B, int T, CiderTables tb,
                                                            const int32_t* img_ref_start, const int32_t* member_batch,
-                                                           const float* lp, int crit, double* fitness_out) {
+                                                           const float* lp, int crit, double* fitness_out,
+                                                           const double* base, double* scores_out) {
     __shared__ double row_score[1024];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int cand = blockIdx.x;
@@ -236,8 +243,10 @@ __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, i
         }
     }
     __syncthreads();
+    if (scores_out)
+        for (int b = threadIdx.x; b < B; b += blockDim.x) scores_out[(size_t)cand * B + b] = row_score[b];
     finish_fitness(row_score, seq + (size_t)cand * B * T, lp ? lp + (size_t)cand * B * T : nullptr, B, T, crit,
-                   fitness_out + cand);
+                   fitness_out + cand, base ? base + (size_t)cand * B : nullptr);
 }
 
 extern "C" uint64_t nicnes_df_hash_capacity(int64_t n) {
@@ -263,10 +272,11 @@ extern "C" hipError_t nicnes_launch_cook_refs(const int32_t* ref_tokens, int n_r
 
 extern "C" hipError_t nicnes_launch_cider(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
                                           const int32_t* img_ref_start, const int32_t* member_batch, const float* lp,
-                                          int crit, double* fitness_out, hipStream_t stream) {
+                                          int crit, double* fitness_out, hipStream_t stream, const double* base,
+                                          double* scores_out) {
     if (B > 1024) return hipErrorInvalidValue;
     hipLaunchKernelGGL(nicnes_cider_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, *tb, img_ref_start,
-                       member_batch, lp, crit, fitness_out);
+                       member_batch, lp, crit, fitness_out, base, scores_out);
     return hipGetLastError();
 }
 
@@ -366,10 +376,10 @@ __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* se
 
 __global__ __launch_bounds__(256) void nicnes_cider_finish_kernel(const int32_t* seq, int B, int T,
                                                                   const double* scores, const float* lp, int crit,
-                                                                  double* fitness_out) {
+                                                                  double* fitness_out, const double* base) {
     const int cand = blockIdx.x;
     finish_fitness(scores + (size_t)cand * B, seq + (size_t)cand * B * T, lp ? lp + (size_t)cand * B * T : nullptr,
-                   B, T, crit, fitness_out + cand);
+                   B, T, crit, fitness_out + cand, base ? base + (size_t)cand * B : nullptr);
 }
 
 extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int B, const CiderTables* tb,
@@ -380,11 +390,12 @@ extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int
 
 extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
                                               const int32_t* img_ref_start, const int32_t* member_batch, const float* lp,
-                                              int crit, double* scores, double* fitness_out, hipStream_t stream) {
+                                              int crit, double* scores, double* fitness_out, hipStream_t stream,
+                                              const double* base) {
     if (B > 1024 || n_cand < 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL(nicnes_cider_img_kernel, dim3(n_cand, (B + CIDER_IMG_ROWS - 1) / CIDER_IMG_ROWS), dim3(256), 0,
                        stream, seq, B, T, *tb, img_ref_start, member_batch, scores);
     hipLaunchKernelGGL(nicnes_cider_finish_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, (const double*)scores,
-                       lp, crit, fitness_out);
+                       lp, crit, fitness_out, base);
     return hipGetLastError();
 }

@@ -13,7 +13,9 @@ struct DecodeParams {
     const float* fc;             // unique-image fc features [images, F]
     const int32_t* member_batch; // nullable: member k of the launch decodes images member_batch[k] * B .. + B
     int32_t* seq;                // out: [members, 2, B, T] greedy tokens (masked after the first 0)
-    float* lp;                   // out (nullable): [members, 2, B, T] log-prob of the greedy token (nets.py:208,241)
+    float* lp;                   // out (nullable): [members, 2, B, T] log-prob of the picked token (nets.py:208,225,241)
+    const double* sample_u;      // nullable: sampled decode (nets.py:210-231, fused path only): the uniform of
+                                 // every (member, sign, row, logit step) [members, 2, B, T]; NULL = greedy
     float* scratch;              // nicnes_decode_scratch_floats(): lane-private c | h' | x0 | unfinished | h' (odd)
     int32_t* stats;              // [0] = exact-pass fallbacks (atomic), [2] = coop hand-off timeouts
     int32_t* alive;              // fused path: [members * slabs], 0 once every row of the workgroup finished

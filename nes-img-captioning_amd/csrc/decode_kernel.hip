@@ -677,6 +677,84 @@ __device__ __forceinline__ void exact_sweep(float* lds, const DecodeParams& p, r
     }
 }
 
+// One sweep of the vocabulary in 32-row tiles for the sampled pick (FCModel._sample with greedy=False,
+// nets.py:210-231; RandomState.choice: the first id whose cumulative probability exceeds the draw): the
+// row's cumulative sum of p = exp((x - m) - lse) in index order, in fp64, against thr = u * sum(p). A lane
+// holds ids 32n + 8k + 4hh + e (k, e < 4): per tile the two lanes of a row exchange their four group sums
+// and walk the eight groups in id order; the lane holding the crossing group walks its four ids. tok /
+// lpv: the pick and its log-prob (logprobs.gather, nets.py:225); V1 - 1 if the sums never reach thr.
+__device__ __forceinline__ void sample_sweep(float* lds, const DecodeParams& p, rsrc_t theta_r, rsrc_t noise_r,
+                                             int tid, int sgn, int hh, int lane, const float (&hB)[64], float m,
+                                             float lse, double thr, int& tok, float& lpv) {
+    const int nvt = (p.V1 + 31) >> 5;
+    auto desc = [&](int n) {
+        TileDesc d;
+        d.w_off = (uint32_t)p.off_log_w; d.ld = 128; d.row0 = 32 * n; d.nvalid = min(32, p.V1 - 32 * n); d.k0 = 0;
+        d.b_off = (uint32_t)p.off_log_b; d.pad_bias = NEG_INF;
+        return d;
+    };
+    StageRegs sr;
+    stage_load(theta_r, noise_r, desc(0), tid, sr);
+    stage_store(lds, desc(0), tid, sr);
+    __syncthreads();
+    double cum = 0.0;
+    bool found = false;
+    int mine = 0x7fffffff;
+    float mlp = 0.f, lastlp = 0.f;
+    for (int n = 0; n < nvt; ++n) {
+        if (n + 1 < nvt) stage_load(theta_r, noise_r, desc(n + 1), tid, sr);
+        const float* buf = lds + (n & 1) * STAGE_FLOATS;
+        const f32x16 acc = mfma_tile(bias_init(buf + 2 * SIGN_FLOATS + 32 * sgn, hh), buf + sgn * SIGN_FLOATS, hB, lane);
+        const int vb = 32 * n + 4 * hh;
+        double g[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            g[k] = 0.0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int v = vb + 8 * k + e;
+                const float x = (acc[4 * k + e] - m) - lse;
+                g[k] += v < p.V1 ? (double)nn_expf(x) : 0.0;
+                if (v == p.V1 - 1) lastlp = x;
+            }
+        }
+        double go[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) go[k] = __shfl_xor(g[k], 32);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {                    // groups in id order: (k, half) = (j >> 1, j & 1)
+            const int k = j >> 1;
+            const bool own = (j & 1) == hh;
+            const double gs = own ? g[k] : go[k];
+            if (!found && cum + gs > thr) {
+                found = true;
+                if (own) {
+                    double c2 = cum;
+                    int pick = vb + 8 * k + 3;
+                    float plp = (acc[4 * k + 3] - m) - lse;
+                    bool hit = false;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float x = (acc[4 * k + e] - m) - lse;
+                        c2 += vb + 8 * k + e < p.V1 ? (double)nn_expf(x) : 0.0;
+                        if (!hit && c2 > thr) { hit = true; pick = vb + 8 * k + e; plp = x; }
+                    }
+                    mine = min(pick, p.V1 - 1);
+                    mlp = plp;
+                }
+            }
+            if (!found) cum += gs;
+        }
+        if (n + 1 < nvt) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), tid, sr);
+        __syncthreads();
+    }
+    const int other = __shfl_xor(mine, 32);
+    const float olp = __shfl_xor(mlp, 32), olast = __shfl_xor(lastlp, 32);
+    if (mine != 0x7fffffff) { tok = mine; lpv = mlp; }
+    else if (other != 0x7fffffff) { tok = other; lpv = olp; }
+    else { tok = p.V1 - 1; lpv = ((p.V1 - 1) & 4) >> 2 == hh ? lastlp : olast; }
+}
+
 // epilogue of one 32-row logit tile (G = 2: one tile per wave); P0 holds vocab vbase + (r&3) + 8(r>>2)
 template <bool PAIRS>
 __device__ __forceinline__ void epilogue32(RowState& st, const f32x16& P0, int vbase) {
@@ -1088,7 +1166,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img64_kernel(DecodePar
 // one step of one workgroup; false when the workgroup is done (every row finished, or t = T).
 // s64 / pre (the steps kernel): staging registers kept across steps; pre says they hold this step's first
 // logit tile, loaded during the previous step's last cell stage (PREFETCH: that load is issued)
-template <bool PAIRS, bool PREFETCH>
+// SAMPLE: the sampled decode (nets.py:210-231): the logit loop keeps only the exact (m, exp-sum), then
+// sample_sweep picks each row's token from its draw p.sample_u (fused path only)
+template <bool PAIRS, bool PREFETCH, bool SAMPLE = false>
 __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, float* lds, int t, Stage64Regs& s64,
                                           bool& pre, float (&hB)[64], bool& hpre) {
     PROF_MARK(2 * (t + 1));
@@ -1142,8 +1222,15 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         const TieWindow w = tie_window(stot, PAIRS, p.lse_margin);
         float lse = w.lse;
         int tok = 0x7fffffff;
+        float lp_tok = 0.f;                      // seq_logprobs: -lse (the max, greedy) or the draw's log-prob
         bool amb = false;
-        {
+        if constexpr (SAMPLE) {
+            const size_t ou = (((size_t)c.member * 2 + c.sgn) * p.B + c.bc) * p.T + (t - 1);
+            const double u = c.row_valid ? p.sample_u[ou] : 0.5;
+            // thr = u * sum over the vocabulary of exp((x - m) - lse) = u * stot * e^-lse
+            const double thr = u * (double)stot * exp(-(double)lse);
+            sample_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, thr, tok, lp_tok);
+        } else {
             const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
             const int ci[4] = {st.r0i, st.r1i, __shfl_xor(st.r0i, 32), __shfl_xor(st.r1i, 32)};
 #pragma unroll
@@ -1152,7 +1239,6 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
                 if (ws == 1 && ci[k] < tok) tok = ci[k];
                 amb = amb || ws == 2;
             }
-        }
         const bool ovf = p.force_exact || amb || win_state(st.ev, m, w) != 0 ||
                          win_state(__shfl_xor(st.ev, 32), m, w) != 0;
         if (__syncthreads_or(ovf ? 1 : 0)) {
@@ -1184,6 +1270,8 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
             }
             if (c.tid == 0) atomicAdd(p.stats + 0, 1);
         }
+        lp_tok = -lse;                           // seq_logprobs[:, t-1] = max lp = fp32((m - m) - lse) (nets.py:208,241)
+        }
         // no candidate only when every logit is NaN (torch.max would return a NaN's index):
         // end the caption instead of emitting an out-of-vocabulary id
         if (tok >= p.V1) tok = 0;
@@ -1195,8 +1283,7 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         if (c.hh == 0 && c.row_valid) {
             const size_t o = (((size_t)c.member * 2 + c.sgn) * p.B + c.b) * p.T + (t - 1);
             p.seq[o] = it;
-            // seq_logprobs[:, t-1] = max lp = fp32((m - m) - lse) = -lse (nets.py:208,241)
-            if (p.lp) p.lp[o] = -lse;
+            if (p.lp) p.lp[o] = lp_tok;
         }
 #endif
         const int any = __syncthreads_or(((unfinished && c.row_valid) || p.no_exit || (DECODE_ABLATE & 64)) ? 1 : 0);
@@ -1314,7 +1401,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
 // workgroup setup; the state between steps stays in the same lane scratch, and a lane re-reads only
 // slots it wrote itself (a same-address store -> load of one lane: ordered like any C++ store/load pair).
 // The LDS stage buffers are free at a step boundary: every step ends on a barrier after its last read.
-template <bool PAIRS>
+template <bool PAIRS, bool SAMPLE = false>
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodeParams p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const Ctx c = make_ctx(p);
@@ -1323,7 +1410,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodePar
     bool pre = false, hpre = false;
     float hB[64];
     for (int t = -1; t <= p.T; ++t)
-        if (!step_body<PAIRS, LOGIT_MIDSTORE && CROSS_PREFETCH>(p, c, lds, t, s64, pre, hB, hpre)) break;
+        if (!step_body<PAIRS, LOGIT_MIDSTORE && CROSS_PREFETCH, SAMPLE>(p, c, lds, t, s64, pre, hB, hpre)) break;
 }
 
 // ========== split path: one member step over several workgroups =================================
@@ -2188,6 +2275,7 @@ extern "C" hipError_t nicnes_decode_init() {
         {(const void*)nicnes_decode_img64_kernel, LDS64},
         {(const void*)nicnes_decode_steps_kernel<true>, LDS64},
         {(const void*)nicnes_decode_steps_kernel<false>, LDS64},
+        {(const void*)nicnes_decode_steps_kernel<false, true>, LDS64},
         {(const void*)nicnes_decode_logit_kernel<4, true>, LDS64},
         {(const void*)nicnes_decode_logit_kernel<4, false>, LDS64},
         {(const void*)nicnes_decode_logit_kernel<2, true>, LDS64},
@@ -2230,6 +2318,7 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
     if (p->G != 4 && p->G != 2) return hipErrorInvalidValue;
     if (p->S < 1 || p->S > 64) return hipErrorInvalidValue;
     if (p->coop && (p->G != 4 || (p->S != 2 && p->S != 4) || !p->coop_ctr)) return hipErrorInvalidValue;
+    if (p->sample_u && (!fused || p->coop)) return hipErrorInvalidValue;     // the sampled pick: fused path only
     const int nl = fused || p->coop ? p->T + 3 : 3 + 2 * p->T;
     if (evs && nl + 1 > DECODE_MAX_EVENTS) return hipErrorInvalidValue;
     int ne = 0;
@@ -2271,7 +2360,10 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
             hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(1, member_count, nslabs), block, LDS32, stream, *p);
         mark(DK_IMG);
         const dim3 grid(member_count, nslabs);
-        if (DECODE_PERSISTENT && !DECODE_PROF) {
+        if (p->sample_u) {                                  // sampled decode: the exact lse, then the draw's pick
+            hipLaunchKernelGGL((nicnes_decode_steps_kernel<false, true>), grid, block, LDS64, stream, *p);
+            mark(DK_STEPS);
+        } else if (DECODE_PERSISTENT && !DECODE_PROF) {
             if (pairs)
                 hipLaunchKernelGGL(nicnes_decode_steps_kernel<true>, grid, block, LDS64, stream, *p);
             else

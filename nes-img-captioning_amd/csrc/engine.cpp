@@ -82,6 +82,10 @@ struct nicnes_handle {
     float* lp = nullptr;              // per-step log-probs for the greedy_* criteria
     double* row_scores = nullptr;     // per-row CIDEr-D of the image-table scorer [2 * max_members, max_batch]
     int fitness_mode = 0;             // nicnes_set_fitness_mode (0 = 'greedy')
+    double* su = nullptr;             // sampled modes: the draws of a decode [count, 2, B, T]
+    double* base_scores = nullptr;    // self-critical modes: the greedy rows' CIDEr-D [2 count, B]
+    int64_t su_cap = 0, base_cap = 0; // ... their capacities (doubles)
+    std::vector<double> su_host;      // nicnes_set_sample_draws (test hook): draws to use instead of the engine's
     float* dscratch = nullptr;
     int32_t* stats = nullptr;
     int32_t* alive = nullptr;         // per decode workgroup: rows left unfinished (fused [stride], split [2][stride])
@@ -400,7 +404,7 @@ int nicnes_destroy(nicnes_handle* h) {
                     h->ref_norm, h->nidx, h->seq, h->lp, h->row_scores, h->dscratch, h->stats, h->partials, h->norms,
                     h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive, h->part,
                     h->rank_key, h->rank_idx, h->mbatch, h->mut_vec, h->dbuf, h->didx, h->noise_sc, h->coop_ctr,
-                    h->zero_noise, h->zero_idx, h->sens_tok};
+                    h->zero_noise, h->zero_idx, h->sens_tok, h->su, h->base_scores};
     if (h->sens) nicnes_sens_destroy(h->sens);
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -634,10 +638,17 @@ int nicnes_set_mutation(nicnes_handle* h, int32_t mode, const float* vec, void* 
     return NICNES_OK;
 }
 
+int nicnes_set_sample_draws(nicnes_handle* h, const double* u_host, int64_t n) {
+    if (!h || n < 0 || (n > 0 && !u_host)) return NICNES_ERR_INVALID;
+    h->su_host.assign(u_host, u_host + n);
+    return NICNES_OK;
+}
+
 int nicnes_set_fitness_mode(nicnes_handle* h, int32_t mode) {
     if (!h) return NICNES_ERR_INVALID;
-    if (mode < NICNES_FITNESS_GREEDY || mode > NICNES_FITNESS_GREEDY_AVGPROB)
-        return fail(h, NICNES_ERR_UNSUPPORTED, "fitness mode: the engine implements greedy and greedy_{log,exp,lin,avg}prob");
+    if (mode < NICNES_FITNESS_GREEDY || mode > NICNES_FITNESS_SC_LOSS)
+        return fail(h, NICNES_ERR_UNSUPPORTED, "fitness mode: the engine implements greedy, greedy_{log,exp,lin,avg}prob, "
+                                               "sample, self_critical and sc_loss");
     h->fitness_mode = mode;
     return NICNES_OK;
 }
@@ -668,10 +679,33 @@ int nicnes_evaluate_lp(nicnes_handle* h, uint64_t iteration, int32_t member_begi
 // eval_theta: the sigma = 0 rollout of theta itself (count 1), decoded ONCE: sign + takes the first half of the
 // batch's images and sign - the second (at sigma = 0 both signs are theta, so the halves are one decode of the
 // batch), scored as one rollout of B rows
+// scores_out (nullable, [n_cand, B]): every rollout row's CIDEr-D (the self-critical modes' greedy baseline)
 static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_begin, int32_t count, float sigma,
                          const int32_t* member_batch_host, double* fitness_out, int32_t* seq_out, float* logprob_out,
-                         void* stream, bool eval_theta) {
+                         void* stream, bool eval_theta, double* scores_out = nullptr) {
     if (!h || !fitness_out || member_begin < 0) return NICNES_ERR_INVALID;
+    const int mode = h->fitness_mode;
+    const bool sampled = mode >= NICNES_FITNESS_SAMPLE;
+    const bool self_critical = mode == NICNES_FITNESS_SELF_CRITICAL || mode == NICNES_FITNESS_SC_LOSS;
+    if (self_critical && !scores_out) {
+        // the greedy decode of the same rollouts first (compute_ciders, policies.py:174-180): its row scores
+        // are the baseline the sampled rows' scores are reduced by
+        const int64_t need = (int64_t)2 * h->cfg.max_members * h->cfg.max_batch;
+        if (need > h->base_cap) {
+            HIPC(h, hipDeviceSynchronize());
+            if (h->base_scores) HIPC(h, hipFree(h->base_scores));
+            h->base_scores = nullptr;
+            h->base_cap = 0;
+            int rc = dalloc(h, &h->base_scores, (size_t)need);
+            if (rc) return rc;
+            h->base_cap = need;
+        }
+        h->fitness_mode = NICNES_FITNESS_GREEDY;
+        const int rc = evaluate_impl(h, iteration, member_begin, count, sigma, member_batch_host, fitness_out, nullptr,
+                                     nullptr, stream, eval_theta, h->base_scores);
+        h->fitness_mode = mode;
+        if (rc) return rc;
+    }
     if (count < 1 || count > h->cfg.max_members) return fail(h, NICNES_ERR_INVALID, "count out of [1, max_members]");
     if (!h->noise) return fail(h, NICNES_ERR_INVALID, "nicnes_set_noise_table first");
     if (!h->theta_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_theta first");
@@ -738,7 +772,10 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     p.fc = h->fc;
     p.member_batch = mb;
     p.seq = seq_out ? seq_out : h->seq;
-    p.lp = logprob_out ? logprob_out : (h->fitness_mode ? h->lp : nullptr);
+    const bool crit_lp = (mode >= NICNES_FITNESS_GREEDY_LOGPROB && mode <= NICNES_FITNESS_GREEDY_AVGPROB) ||
+                         mode == NICNES_FITNESS_SC_LOSS;                // the criterion needs seq_logprobs
+    p.lp = logprob_out ? logprob_out : (crit_lp ? h->lp : nullptr);
+    p.sample_u = nullptr;
     p.scratch = h->dscratch;
     p.stats = h->stats;
     p.alive = h->alive;
@@ -759,12 +796,36 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     const int rows = eval_theta ? (h->B + 1) / 2 : h->B;
     int G = 0, nslabs = 0, S = 0;
     decode_shape(h, rows, count, &G, &nslabs, &S);
+    if (sampled) {          // the sampled pick runs on the fused path (128-row slabs, one workgroup per slab)
+        G = 4;
+        S = 1;
+        nslabs = nslabs_of(rows, 4);
+        const int64_t need = (int64_t)count * 2 * rows * h->cfg.seq_length;
+        if (need > h->su_cap) {
+            HIPC(h, hipDeviceSynchronize());
+            if (h->su) HIPC(h, hipFree(h->su));
+            h->su = nullptr;
+            h->su_cap = 0;
+            int rc = dalloc(h, &h->su, (size_t)need);
+            if (rc) return rc;
+            h->su_cap = need;
+        }
+        if (!h->su_host.empty()) {
+            if ((int64_t)h->su_host.size() != need)
+                return fail(h, NICNES_ERR_INVALID, "nicnes_set_sample_draws: count x 2 x B x seq_length draws needed");
+            HIPC(h, hipMemcpyAsync(h->su, h->su_host.data(), (size_t)need * sizeof(double), hipMemcpyHostToDevice, s));
+        } else {
+            HIPC(h, nicnes_launch_sample_draws(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, rows,
+                                               h->cfg.seq_length, h->su, s));
+        }
+        p.sample_u = h->su;
+    }
     if ((int64_t)count * nslabs * S > h->part_cap)
         return fail(h, NICNES_ERR_INVALID, "decode split beyond the partial-state buffer (nicnes_set_decode_split)");
     p.G = G;
     p.S = S;
     p.part = h->part;
-    p.coop = coop_fits(h, G, nslabs, S, count) ? 1 : 0;
+    p.coop = !sampled && coop_fits(h, G, nslabs, S, count) ? 1 : 0;
     // log-probs of a batch spread over several slabs: every slab runs to T, then the steps after the
     // batch's last finishing step are zeroed (nicnes_lp_batch_exit), as FCModel._sample leaves them
     p.no_exit = (p.lp && nslabs > 1) ? 1 : 0;
@@ -834,12 +895,17 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     }
     CiderTables tb = tables_of(h);
     const int n_cand = eval_theta ? 1 : 2 * count;      // eval_theta: rows s * half + b = image s * half + b
-    if (h->img_tables)
+    const double* base = self_critical ? h->base_scores : nullptr;
+    if (h->img_tables) {
         HIPC(h, nicnes_launch_cider_img(p.seq, n_cand, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
-                                         h->fitness_mode, h->row_scores, fitness_out, s));
-    else
+                                         h->fitness_mode, h->row_scores, fitness_out, s, base));
+        if (scores_out)
+            HIPC(h, hipMemcpyAsync(scores_out, h->row_scores, (size_t)n_cand * h->B * sizeof(double),
+                                   hipMemcpyDeviceToDevice, s));
+    } else {
         HIPC(h, nicnes_launch_cider(p.seq, n_cand, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
-                                    h->fitness_mode, fitness_out, s));
+                                    h->fitness_mode, fitness_out, s, base, scores_out));
+    }
     if (h->timing) HIPC(h, hipEventRecord(h->ev[2], s));
     return NICNES_OK;
 }
@@ -896,6 +962,7 @@ int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, floa
     p.part = h->part;
     p.coop_ctr = h->coop_ctr;
     p.coop = 0;
+    p.sample_u = nullptr;
     p.force_exact = h->force_exact;
     p.lse_margin = h->lse_margin;
     p.bounded_lse = 1;

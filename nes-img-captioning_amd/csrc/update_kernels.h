@@ -26,6 +26,8 @@ struct AdamParams {
 
 extern "C" hipError_t nicnes_launch_noise_index(uint64_t seed, uint64_t iteration, uint64_t member0, int count,
                                                 uint64_t table_len, uint64_t dim, uint64_t* out, hipStream_t s);
+extern "C" hipError_t nicnes_launch_sample_draws(uint64_t seed, uint64_t iteration, uint64_t member0, int count, int B,
+                                                 int T, double* out, hipStream_t s);
 extern "C" hipError_t nicnes_launch_noise_vectors(const float* noise, const uint64_t* idx, int count, int64_t dim,
                                                   float sigma, float* out, hipStream_t s);
 extern "C" hipError_t nicnes_launch_mutate(const float* noise, const uint64_t* idx, int count, int64_t dim, float sigma,

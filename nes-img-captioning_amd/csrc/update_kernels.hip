@@ -10,6 +10,7 @@
 //                          master's g' = -g + l2coeff*theta (nic_nes_master.py:126,133), fp64 state,
 //                          evaluated with the same IEEE op sequence numpy uses (no fma contraction)
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 
 #include "../../include/nicnes_math.h"
@@ -246,6 +247,30 @@ extern "C" hipError_t nicnes_launch_noise_index(uint64_t seed, uint64_t iteratio
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(nicnes_noise_index_kernel, dim3((count + 255) / 256), dim3(256), 0, s, seed, iteration, member0,
                        count, table_len, dim, out);
+    return hipGetLastError();
+}
+
+// the uniforms of a sampled decode (RandomState.choice's one random_sample per row and logit step,
+// nets.py:220-224): u of (member member0 + k, sign s, row b, step t) from a counter-based hash of the
+// noise seed, the iteration and those coordinates, 53-bit like numpy's random_sample; [count, 2, B, T]
+__global__ void nicnes_sample_draws_kernel(uint64_t seed, uint64_t iteration, uint64_t member0, int count, int B,
+                                           int T, double* out) {
+    const int64_t n = (int64_t)count * 2 * B * T;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = i / (2 * (int64_t)B * T), r = i % (2 * (int64_t)B * T);
+        const uint64_t key = nn_splitmix64(seed ^ 0x6a09e667f3bcc909ull ^ ((iteration << 32) | (member0 + (uint64_t)k)));
+        const uint64_t x = nn_splitmix64(key ^ (uint64_t)r);
+        out[i] = (double)(x >> 11) * (1.0 / 9007199254740992.0);
+    }
+}
+
+extern "C" hipError_t nicnes_launch_sample_draws(uint64_t seed, uint64_t iteration, uint64_t member0, int count, int B,
+                                                 int T, double* out, hipStream_t s) {
+    const int64_t n = (int64_t)count * 2 * B * T;
+    if (n <= 0) return hipSuccess;
+    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(nicnes_sample_draws_kernel, dim3(blocks), dim3(256), 0, s, seed, iteration, member0, count, B, T,
+                       out);
     return hipGetLastError();
 }
 

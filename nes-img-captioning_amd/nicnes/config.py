@@ -6,8 +6,8 @@ Field names and defaults mirror
   ModelOptions      /root/reference/src/algorithm/policies.py:36-41
   optimizer_options /root/reference/src/algorithm/nic_nes/experiment.py:20-21
 A leading underscore disables a key ("_from_infos"), as in the reference JSON files. The engine
-implements the mscoco_nes.json hot path only: net 'fc_caption', fitness 'greedy' or one of the
-greedy_* criteria (greedy_logprob / expprob / linprob / avgprob), model_options.safe_mutations
+implements the mscoco_nes.json hot path only: net 'fc_caption', every Fitness value (greedy, the
+greedy_* criteria, and the sampled sample / self_critical / sc_loss), model_options.safe_mutations
 '' / SM-G-SUM / SM-VECTOR / SM-PROPORTIONAL (nicnes.mutations), no vbn / layer_n; anything else
 raises NotSupported (nicnes_create returns NICNES_ERR_UNSUPPORTED for unsupported model sizes).
 """
@@ -37,6 +37,8 @@ ModelOptions = namedtuple('ModelOptions', field_names=_model_opt_fields, default
 # Fitness modes the engine implements: greedy decoding, scored by CIDEr-D alone or by a criterion
 # over the greedy tokens' log-probs (Fitness.is_greedy, src/captioning/policies.py:45-47)
 GREEDY_FITNESS = ('greedy', 'greedy_logprob', 'greedy_expprob', 'greedy_linprob', 'greedy_avgprob')
+SAMPLED_FITNESS = ('sample', 'self_critical', 'sc_loss')
+FITNESS = GREEDY_FITNESS + SAMPLED_FITNESS          # every Fitness enum value (src/captioning/policies.py:22-35)
 
 
 class NotSupported(ValueError):
@@ -81,9 +83,9 @@ class ExperimentSpec:
         po, mo = self.policy_options, self.model_options
         if po.net != 'fc_caption':
             raise NotSupported('net %r: the engine implements fc_caption' % po.net)
-        if self.fitness not in GREEDY_FITNESS:
+        if self.fitness not in FITNESS:
             raise NotSupported("fitness %r: the engine implements %s (src/captioning/policies.py:22-61)"
-                               % (po.fitness, ', '.join(GREEDY_FITNESS)))
+                               % (po.fitness, ', '.join(FITNESS)))
         if po.vbn or mo.vbn_e or mo.layer_n:
             raise NotSupported('virtual batch norm / layer norm are not implemented by the engine')
         m = self.mutation

@@ -197,7 +197,8 @@ class Engine:
 
     # Fitness enum values the engine implements (src/captioning/policies.py:22-35) -> nicnes.h codes
     FITNESS_MODES = {'greedy': 0, 'greedy_logprob': 1, 'greedy_expprob': 2, 'greedy_linprob': 3,
-                     'greedy_avgprob': 4}
+                     'greedy_avgprob': 4, 'sample': 5, 'self_critical': 6, 'sc_loss': 7}
+    SAMPLED_MODES = (5, 6, 7)
 
     def set_fitness_mode(self, fitness):
         """Fitness criterion by its experiment-JSON name (policy_options.fitness) or nicnes.h code."""
@@ -230,6 +231,18 @@ class Engine:
                                                  self._stream()), self.h, 'evaluate')
         out = (fit,) + ((seq,) if return_seq else ()) + ((lp,) if return_lp else ())
         return out if len(out) > 1 else fit
+
+    def set_sample_draws(self, u=None):
+        """Test hook: the uniforms [count, 2, B, T] fp64 the next sampled evaluates use (None: the engine's
+        own counter-based draws)."""
+        if u is None:
+            check(self.L.nicnes_set_sample_draws(self.h, None, 0), self.h, 'set_sample_draws')
+            self._keep.pop('draws', None)
+            return
+        a = np.ascontiguousarray(np.asarray(u, np.float64))
+        check(self.L.nicnes_set_sample_draws(self.h, a.ctypes.data_as(ctypes.c_void_p), a.size), self.h,
+              'set_sample_draws')
+        self._keep['draws'] = a
 
     def evaluate_theta(self, batch=0, return_seq=False, return_lp=False):
         """Fitness of theta itself on the batch held (or batch `batch` of set_batches'): the sigma = 0

@@ -20,7 +20,7 @@ import time
 import numpy as np
 import torch
 
-from .nes import NESTask, make_optimizer, state_dict_from_vector, param_shapes, EnginePolicy, unique_batch
+from .nes import NESTask, make_optimizer, state_dict_from_vector, param_shapes, EnginePolicy, engine_batch
 from .population import PopulationRunner
 
 
@@ -109,14 +109,14 @@ class EngineMaster:
         can be reused by the next one."""
         if batch is not self._batch_key:
             if isinstance(batch, list):
-                ub = [unique_batch(b) if isinstance(b, dict) else b for b in batch]
+                ub = [engine_batch(b, self.e) if isinstance(b, dict) else b for b in batch]
                 if len(ub) == 1:
                     self.e.set_batch(*ub[0])
                 else:
                     self.e.set_batches(ub)
                 self._n_batches = len(ub)
             else:
-                fc, gts = unique_batch(batch) if isinstance(batch, dict) else batch
+                fc, gts = engine_batch(batch, self.e) if isinstance(batch, dict) else batch
                 self.e.set_batch(fc, gts)
                 self._n_batches = 1
             self._batch_key = batch

@@ -77,6 +77,29 @@ def unique_batch(data, seq_per_img=5):
     return np.ascontiguousarray(fc), gts
 
 
+SAMPLED_FITNESS_CODES = (5, 6, 7)     # 'sample', 'self_critical', 'sc_loss' (nicnes.h NICNES_FITNESS_*)
+
+
+def sampled_batch(data, seq_per_img=5):
+    """Reference batch dict -> (fc [B*seq_per_img, F], gts per row): every row the reference decodes.
+    Sampled decoding (FCModel._sample, greedy=False) draws each duplicated row independently, so the rows
+    are kept and row i scores against image i // seq_per_img (compute_ciders, policies.py:161-170)."""
+    fc = np.ascontiguousarray(np.asarray(data['fc_feats'], np.float32))
+    gts = data['gts']
+    spi = fc.shape[0] // len(gts)
+    if spi * len(gts) != fc.shape[0]:
+        raise ValueError('fc_feats rows (%d) are not a multiple of the %d images of gts' % (fc.shape[0], len(gts)))
+    return fc, [gts[i // spi] for i in range(fc.shape[0])]
+
+
+def engine_batch(data, engine, seq_per_img=5):
+    """The rows the engine decodes for its fitness mode: one per image for the greedy modes (unique_batch),
+    all of them for the sampled modes (sampled_batch)."""
+    if getattr(engine, 'fitness_mode', 0) in SAMPLED_FITNESS_CODES:
+        return sampled_batch(data, seq_per_img)
+    return unique_batch(data, seq_per_img)
+
+
 def member_batches(batch_data, member_begin, count):
     """Per-member batch indices when batch_data is a list of G batches (member i uses batch i mod G),
     None for one shared batch."""
@@ -137,14 +160,14 @@ class EnginePolicy:
         can be reused by the next one."""
         if data is not self._batch_key:
             if isinstance(data, (list, tuple)):
-                ub = [unique_batch(d, seq_per_img) for d in data]
+                ub = [engine_batch(d, self.e, seq_per_img) for d in data]
                 if len(ub) == 1:
                     self.e.set_batch(*ub[0])
                 else:
                     self.e.set_batches(ub)
                 rows = ub[0][0].shape[0]
             else:
-                fc, gts = unique_batch(data, seq_per_img)
+                fc, gts = engine_batch(data, self.e, seq_per_img)
                 self.e.set_batch(fc, gts)
                 rows = fc.shape[0]
             self._batch_key = data
@@ -153,7 +176,8 @@ class EnginePolicy:
 
     def rollout(self, placeholder, data, config):
         """CaptPolicy.rollout (policies.py:86-128) of the current theta: float(100 * mean CIDEr-D) for
-        'greedy', the criterion value for the greedy_* fitness modes."""
+        'greedy' and 'sample', 100 * the mean self-critical difference for 'self_critical', the criterion
+        value for the greedy_* modes and 'sc_loss'."""
         self._ensure_batch(data)
         # theta itself, decoded once (nicnes_evaluate_theta: the two antithetic signs split the images);
         # with several batches held, member 0's batch (member_batches' rule)

@@ -56,7 +56,7 @@ def test_spec_reads_mscoco_nes():
 
 
 @pytest.mark.parametrize('over', [
-    {'policy_options': {'net': 'fc_caption', 'fitness': 'sample'}},
+    {'policy_options': {'net': 'fc_caption', 'fitness': 'beam'}},
     {'policy_options': {'net': 'att_caption'}},
     {'policy_options': {'net': 'fc_caption', 'vbn': True}},
     {'policy_options': {'net': 'fc_caption', 'model_options': {'safe_mutations': 'SM-G-ABS'}}},
@@ -70,9 +70,9 @@ def test_spec_rejects_unsupported(over):
 
 
 @pytest.mark.parametrize('fitness', ['greedy', 'greedy_logprob', 'greedy_expprob', 'greedy_linprob',
-                                     'greedy_avgprob', None])
-def test_spec_accepts_greedy_fitness_modes(fitness):
-    """Fitness.is_greedy modes (src/captioning/policies.py:45-47); None -> Fitness.DEFAULT 'greedy'."""
+                                     'greedy_avgprob', 'sample', 'self_critical', 'sc_loss', None])
+def test_spec_accepts_fitness_modes(fitness):
+    """Every Fitness value (src/captioning/policies.py:22-35); None -> Fitness.DEFAULT 'greedy'."""
     s = C.ExperimentSpec(_exp(policy_options={'net': 'fc_caption', 'fitness': fitness}))
     assert s.fitness == (fitness or 'greedy')
 

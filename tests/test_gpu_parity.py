@@ -194,7 +194,7 @@ def test_set_batch_rejects_images_without_references(eng):
 
 def test_fitness_mode_rejects_unsupported(eng):
     import nicnes
-    for bad in ('sample', 'self_critical', 'sc_loss', 7):
+    for bad in ('beam', 8, -1):
         with pytest.raises((nicnes.NicnesError, ValueError, RuntimeError)):
             eng.set_fitness_mode(bad)
     eng.set_fitness_mode('greedy')

@@ -1,0 +1,190 @@
+"""GPU: the sampled fitness modes (Fitness 'sample', 'self_critical', 'sc_loss',
+/root/reference/src/captioning/policies.py:22-61,86-193) and their decode, FCModel._sample with
+greedy=False (nets.py:210-231: each row draws its token from the softmax with one uniform per row and
+logit step), through the C ABI.
+
+Parity: with the draws the reference itself took (tests/golden/decode_sample.npz, replayed numpy
+RandomState draws, scripts/make_golden.py) the engine's tokens equal the reference's on every row up to
+its first draw within 1e-6 of a cdf boundary (the order p is summed in moves the boundaries by ~1e-7),
+and the oracle's (oracle.decode_sample) the same way; fitness against the CIDEr-D / criterion oracle."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O          # noqa: E402
+from oracle import cider_ref as CR      # noqa: E402
+from tests.test_oracle_golden import sample_case, U_MARGIN   # noqa: E402
+
+NOISE_LEN = 1 << 23
+SIGMA = 0.01
+
+
+@pytest.fixture(scope='module')
+def eng():
+    import nicnes
+    assert torch.cuda.is_available(), 'GPU tests need a GPU'
+    e = nicnes.Engine(max_batch=128, max_members=4, noise_len=NOISE_LEN, noise_seed=7)
+    table = O.noise_table(NOISE_LEN, 123)
+    e.set_noise_table(table)
+    e._table_np = table
+    yield e
+    e.close()
+
+
+def _load(eng, theta, fc, seed=11, n_refs=5):
+    import nicnes
+    import nicnes.synthetic as S
+    dims = O.Dims()
+    base, _, _ = O.decode(dims, theta, fc)
+    gts, df, n = S.build_references(base, dims.vocab_size, seed=seed, n_refs=n_refs, df_sets=256)
+    eng.set_theta(theta)
+    keys, vals = nicnes.df_table_arrays(df)
+    eng.set_df_table(keys, vals, np.log(float(n)))
+    eng.set_batch(fc, gts)
+    return gts, CR.CiderDOracle(df, n)
+
+
+def _rows_agree(got, want, stop):
+    """tokens equal on each row up to (excluding) its first step where stop[b, t]"""
+    n = 0
+    for b in range(want.shape[0]):
+        for t in range(want.shape[1]):
+            if stop[b, t]:
+                break
+            assert got[b, t] == want[b, t], (b, t, got[b], want[b])
+            n += 1
+    return n
+
+
+@pytest.mark.parametrize('name', ['full_xavier', 'full_wc'])
+def test_sampled_decode_matches_reference(eng, name):
+    """theta itself (sigma = 0, both signs) with the reference's draws: tokens = the reference's and the
+    oracle's, sampled log-probs (seq_logprobs) to 5e-6 of the reference's."""
+    golden = '%s/golden' % __import__('os').path.dirname(__file__)
+    d, theta, fc, g = sample_case(golden, name)
+    _load(eng, theta, fc)
+    eng.set_fitness_mode('sample')
+    try:
+        eng.set_sample_draws(np.stack([g['u'], g['u']])[None])
+        _, seq, lp = eng.evaluate(1, 0, 1, 0.0, return_seq=True, return_lp=True)
+    finally:
+        eng.set_sample_draws(None)
+        eng.set_fitness_mode('greedy')
+    seq, lp = seq.cpu().numpy(), lp.cpu().numpy()
+    oseq, olp, ofr = O.decode_sample(d, theta, fc, g['u'])
+    for s in range(2):
+        stop = (g['u_margin'] < U_MARGIN) | (ofr != 0)
+        n = _rows_agree(seq[0, s], g['seq'], stop)
+        assert n >= 0.8 * seq[0, s].size, n
+        _rows_agree(seq[0, s], oseq, ofr != 0)
+        live = (~np.cumsum(stop, axis=1).astype(bool)) & (g['logprobs'] != 0)
+        assert np.allclose(lp[0, s][live], g['logprobs'][live], rtol=5e-6, atol=5e-6)
+
+
+def test_sampled_members_match_oracle(eng):
+    """perturbed members (theta +- sigma z), seeded draws, one and two slabs: tokens = the oracle's up to the
+    first fragile draw; 'sample' fitness = 100 * mean CIDEr-D of the sampled rows (1e-9 relative)."""
+    dims = O.Dims()
+    theta = O.make_theta(dims, 0, 4.0, 0.1)
+    for B in (40, 130):                                     # 130 rows: two 128-row slabs
+        fc = np.random.Generator(np.random.PCG64(B)).standard_normal((B, dims.F)).astype(np.float32)
+        gts, scorer = _load(eng, theta, fc)
+        u = np.random.Generator(np.random.PCG64(5)).random((3, 2, B, dims.T))
+        eng.set_fitness_mode('sample')
+        try:
+            eng.set_sample_draws(u)
+            fit, seq = eng.evaluate(4, 0, 3, SIGMA, return_seq=True)
+        finally:
+            eng.set_sample_draws(None)
+            eng.set_fitness_mode('greedy')
+        fit, seq = fit.cpu().numpy(), seq.cpu().numpy()
+        idx = eng.noise_indices(4, 0, 3).cpu().numpy()
+        for k in range(3):
+            for s, sign in enumerate((+1, -1)):
+                oseq, _, ofr = O.decode_sample(dims, O.perturb(theta, eng._table_np, int(idx[k]), SIGMA, sign), fc,
+                                               u[k, s])
+                _rows_agree(seq[k, s], oseq, ofr != 0)
+                f_ref, _ = CR.rollout_fitness(scorer, seq[k, s], gts)
+                assert abs(fit[k, s] - f_ref) <= 1e-9 * max(1.0, abs(f_ref)), (k, s, fit[k, s], f_ref)
+
+
+def test_self_critical_and_sc_loss(eng):
+    """'self_critical' = 100 * mean(sampled row score - greedy row score) = f_sample - f_greedy;
+    'sc_loss' = LogFitnessCriterion (fitness.py:12-40) of the sampled log-probs with those per-row
+    differences as rewards (the criterion oracle is pinned by tests/golden/fitness_criteria.npz)."""
+    dims = O.Dims()
+    theta = O.make_theta(dims, 0, 4.0, 0.1)
+    B = 40
+    fc = np.random.Generator(np.random.PCG64(9)).standard_normal((B, dims.F)).astype(np.float32)
+    gts, scorer = _load(eng, theta, fc)
+    u = np.random.Generator(np.random.PCG64(6)).random((2, 2, B, dims.T))
+    out = {}
+    try:
+        eng.set_sample_draws(u)
+        for mode in ('greedy', 'sample', 'self_critical', 'sc_loss'):
+            eng.set_fitness_mode(mode)
+            if mode == 'sc_loss':
+                out[mode] = tuple(x.cpu().numpy() for x in eng.evaluate(3, 0, 2, SIGMA, return_seq=True,
+                                                                        return_lp=True))
+            else:
+                out[mode] = tuple(x.cpu().numpy() for x in eng.evaluate(3, 0, 2, SIGMA, return_seq=True))
+    finally:
+        eng.set_sample_draws(None)
+        eng.set_fitness_mode('greedy')
+    fg, sg = out['greedy']
+    fs, ss = out['sample']
+    fsc, ssc = out['self_critical']
+    fl, sl, lpl = out['sc_loss']
+    assert np.array_equal(ss, ssc) and np.array_equal(ss, sl)          # the same draws, the same samples
+    assert np.allclose(fsc, fs - fg, rtol=0, atol=1e-9), (fsc, fs - fg)
+    for k in range(2):
+        for s in range(2):
+            _, sc_s = CR.rollout_fitness(scorer, ss[k, s], gts)
+            _, sc_g = CR.rollout_fitness(scorer, sg[k, s], gts)
+            want = CR.criterion_fitness('sc_loss', lpl[k, s], sl[k, s], np.asarray(sc_s) - np.asarray(sc_g))
+            assert abs(fl[k, s] - want) <= 1e-6 * max(1.0, abs(want)), (k, s, fl[k, s], want)
+    assert fs.max() > 0.0
+
+
+def test_engine_draws_are_deterministic_per_iteration(eng):
+    """the engine's own draws (no hook): a counter-based hash of (seed, iteration, member, sign, row, step):
+    the same iteration repeats exactly, another iteration samples other captions."""
+    dims = O.Dims()
+    theta = O.make_theta(dims, 0, 1.0, 0.0)
+    fc = np.random.Generator(np.random.PCG64(3)).standard_normal((24, dims.F)).astype(np.float32)
+    _load(eng, theta, fc)
+    eng.set_fitness_mode('sample')
+    try:
+        a = eng.evaluate(5, 0, 2, SIGMA, return_seq=True)[1].cpu().numpy()
+        b = eng.evaluate(5, 0, 2, SIGMA, return_seq=True)[1].cpu().numpy()
+        c = eng.evaluate(6, 0, 2, SIGMA, return_seq=True)[1].cpu().numpy()
+        d = eng.evaluate(5, 1, 1, SIGMA, return_seq=True)[1].cpu().numpy()
+    finally:
+        eng.set_fitness_mode('greedy')
+    assert np.array_equal(a, b) and not np.array_equal(a, c)
+    assert np.array_equal(a[1], d[0])                                  # member 1 draws the same alone
+    assert len(np.unique(a[:, :, :, 0])) > 10                          # flat xavier logits: many first words
+
+
+def test_policy_keeps_duplicated_rows_for_sampled_modes(eng):
+    """EnginePolicy.rollout with 'sample': the 5 duplicated rows of each image are decoded (each draws its
+    own tokens, dataloader.py:175), greedy modes decode one row per image."""
+    import nicnes.nes as N
+    dims = O.Dims()
+    theta = O.make_theta(dims, 0, 1.0, 0.0)
+    fc = np.random.Generator(np.random.PCG64(3)).standard_normal((8, dims.F)).astype(np.float32)
+    gts, _ = _load(eng, theta, fc)
+    data = {'fc_feats': np.repeat(fc, 5, 0), 'gts': gts}
+    pol = N.EnginePolicy(eng)
+    eng.set_fitness_mode('sample')
+    try:
+        f = pol.rollout(None, data, None)
+        assert eng.B == 40 and np.isfinite(f)
+    finally:
+        eng.set_fitness_mode('greedy')
+    pol._batch_key = None
+    pol.rollout(None, data, None)
+    assert eng.B == 8
