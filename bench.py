@@ -188,8 +188,10 @@ def main():
     ap.add_argument('--noise-len', type=int, default=1 << 27)
     ap.add_argument('--bu', action='store_true', help="'bu' features: ReLU(N(0,1)) fc (configs[4]; implied by "
                     "--preset configs4)")
-    ap.add_argument('--fitness', default='greedy', help="policy_options.fitness: greedy (mscoco_nes.json) or "
-                    "greedy_logprob / greedy_expprob / greedy_linprob / greedy_avgprob")
+    ap.add_argument('--fitness', default='greedy', help="policy_options.fitness: greedy (mscoco_nes.json), "
+                    "greedy_logprob / greedy_expprob / greedy_linprob / greedy_avgprob, or the sampled sample / "
+                    "self_critical / sc_loss (every one of the batch's 5 rows per image decoded: the rows the "
+                    "reference samples independently)")
     ap.add_argument('--mutation', default='', choices=['', 'SM-G-SUM', 'SM-PROPORTIONAL'],
                     help="model_options.safe_mutations (mscoco_nes.json: '', underflow 0.1): the per-task mutation "
                     "vector is recomputed from each iteration's theta on the host (nicnes.mutations) inside the "
@@ -237,10 +239,16 @@ def main():
             dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
         else:
             dist.init_process_group(backend)
-    eng = nicnes.Engine(max_batch=B, max_members=P_local, noise_len=args.noise_len, noise_seed=0,
+    sampled = args.fitness in ('sample', 'self_critical', 'sc_loss')
+    spi = 5 if sampled else 1               # sampled modes decode the reference's seq_per_img copies of each image
+    eng = nicnes.Engine(max_batch=B * spi, max_members=P_local, noise_len=args.noise_len, noise_seed=0,
                         device=dev)
     wl = S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu, batches=args.batches,
                                  theta_gain=args.theta_gain, bias_std=args.bias_std)
+    if sampled:
+        if args.batches > 1:
+            raise SystemExit('--fitness %s with --batches: not supported by this bench' % args.fitness)
+        eng.set_batch(np.repeat(wl['fc'], spi, 0), [g for g in wl['gts'] for _ in range(spi)])
     eng.set_fitness_mode(args.fitness)
     eng.set_decode_split(args.decode_split, args.decode_rows)
     runner = PopulationRunner(eng, P, args.sigma, l2coeff=1e-7, stepsize=1e-3, rank=rank, world_size=world,
@@ -304,7 +312,17 @@ def main():
     ph = phases[-1]
     G, nslabs, S_split = eng.decode_shape(B, P_local)
     path = eng.decode_path(B, P_local)
-    if not ph['step_launches'] and not ph['logit_launches']:
+    if sampled:
+        # the sampled decode of the 5 B rows: the steps kernel (exact lse) + a second logit sweep per step for the
+        # draw's pick, one launch; the self-critical modes' greedy decode runs before it (in ms_per_step, not here)
+        rows = B * spi
+        G, nslabs, S_split, path = 4, (rows + 127) // 128, 1, 'fused (sampled pick)'
+        kname, n_step = 'nicnes_decode_steps_kernel<sample>', 1
+        step_ms = float(np.mean([q['step_ms'] for q in phases]))
+        flops = (decode_flops_per_member(rows) + logit_flops_per_member(rows)) * P_local
+        step_flop = (step_flops_per_member(rows) + logit_flops_per_member(rows)) * P_local
+        alg_bytes = (step_noise_bytes_per_member(rows) + 16 * logit_noise_bytes_per_member()) * P_local
+    elif not ph['step_launches'] and not ph['logit_launches']:
         # two-stream decode (NICNES_DECODE_STREAMS=2): the halves' launches overlap, so the whole decode
         # is the measured unit
         kname, n_step = 'decode (img + step/logit/cell kernels, 2 streams)', 1
@@ -349,6 +367,7 @@ def main():
                                'images, sigma %.3g, full iteration (decode+CIDEr-D+ranks+noise sum+Adam)'
                                % (P, P_local, scaling, B, args.sigma) + (", 'bu' fc features" if args.bu else '')
                                + (', fitness %s' % args.fitness if args.fitness != 'greedy' else '')
+                               + (' (%d rows per rollout: 5 sampled per image)' % (B * spi) if sampled else '')
                                + (', theta gain %g bias std %g (not the reference init)' % (args.theta_gain, args.bias_std)
                                   if (args.theta_gain != 1.0 or args.bias_std) else '')
                                + (', %d batches per iteration (single_batch false: member i on batch i mod %d)'
