@@ -188,3 +188,48 @@ def test_policy_keeps_duplicated_rows_for_sampled_modes(eng):
     pol._batch_key = None
     pol.rollout(None, data, None)
     assert eng.B == 8
+
+
+def test_sampled_with_member_batches_and_mutation(eng):
+    """the sampled decode follows the member -> batch map (single_batch: false) and reads a mutation's
+    delta' rows (SM-PROPORTIONAL) like the greedy decode: tokens against the oracle up to the first
+    fragile draw, 'sample' fitness against the CIDEr-D oracle on each member's batch."""
+    import nicnes
+    import nicnes.synthetic as S
+    dims = O.Dims()
+    theta = O.make_theta(dims, 1, 4.0, 0.1)
+    B = 24
+    batches = []
+    for j in range(2):
+        fc = np.random.Generator(np.random.PCG64(40 + j)).standard_normal((B, dims.F)).astype(np.float32)
+        base, _, _ = O.decode(dims, theta, fc)
+        gts, df, n = S.build_references(base, dims.vocab_size, seed=50 + j, df_sets=256)
+        batches.append((fc, gts))
+    eng.set_theta(theta)
+    keys, vals = nicnes.df_table_arrays(df)
+    eng.set_df_table(keys, vals, np.log(float(n)))
+    eng.set_batches(batches)
+    scorer = CR.CiderDOracle(df, n)
+    vec = np.abs(theta).astype(np.float32)
+    vec[vec == 0] = np.abs(theta).mean()
+    u = np.random.Generator(np.random.PCG64(8)).random((2, 2, B, dims.T))
+    mb = [1, 0]
+    eng.set_fitness_mode('sample')
+    try:
+        eng.set_mutation('scale', vec)                       # SM-PROPORTIONAL: delta * |theta'|
+        eng.set_sample_draws(u)
+        fit, seq = eng.evaluate(3, 0, 2, SIGMA, return_seq=True, member_batch=mb)
+    finally:
+        eng.set_sample_draws(None)
+        eng.set_mutation('plain')
+        eng.set_fitness_mode('greedy')
+    fit, seq = fit.cpu().numpy(), seq.cpu().numpy()
+    idx = eng.noise_indices(3, 0, 2).cpu().numpy()
+    for k in range(2):
+        fc, gts = batches[mb[k]]
+        for s, sign in enumerate((+1, -1)):
+            th = O.perturb(theta, eng._table_np, int(idx[k]), SIGMA, sign, ('scale', vec))
+            oseq, _, ofr = O.decode_sample(dims, th, fc, u[k, s])
+            _rows_agree(seq[k, s], oseq, ofr != 0)
+            f_ref, _ = CR.rollout_fitness(scorer, seq[k, s], gts)
+            assert abs(fit[k, s] - f_ref) <= 1e-9 * max(1.0, abs(f_ref)), (k, s)
