@@ -241,15 +241,12 @@ def main():
             dist.init_process_group(backend)
     sampled = args.fitness in ('sample', 'self_critical', 'sc_loss')
     spi = 5 if sampled else 1               # sampled modes decode the reference's seq_per_img copies of each image
-    eng = nicnes.Engine(max_batch=B * spi, max_members=P_local, noise_len=args.noise_len, noise_seed=0,
-                        device=dev)
+    eng = nicnes.Engine(max_batch=B, max_members=P_local, noise_len=args.noise_len, noise_seed=0, device=dev)
     wl = S.setup_engine_workload(eng, B=B, fc_seed=1235 if args.bu else 1234, bu=args.bu, batches=args.batches,
                                  theta_gain=args.theta_gain, bias_std=args.bias_std)
-    if sampled:
-        if args.batches > 1:
-            raise SystemExit('--fitness %s with --batches: not supported by this bench' % args.fitness)
-        eng.set_batch(np.repeat(wl['fc'], spi, 0), [g for g in wl['gts'] for _ in range(spi)])
     eng.set_fitness_mode(args.fitness)
+    if sampled:
+        eng.set_rows_per_image(spi)          # each image's 5 copies decoded, each with its own draws
     eng.set_decode_split(args.decode_split, args.decode_rows)
     runner = PopulationRunner(eng, P, args.sigma, l2coeff=1e-7, stepsize=1e-3, rank=rank, world_size=world,
                               group=group)

@@ -140,6 +140,13 @@ int nicnes_set_mutation(nicnes_handle* h, int32_t mode, const float* vec, void* 
 #define NICNES_FITNESS_SC_LOSS 7          /* 'sc_loss': LogFitnessCriterion */
 int nicnes_set_fitness_mode(nicnes_handle* h, int32_t mode);
 
+/* Rows per image of the sampled modes: each image of the batch is decoded n times (the reference's
+ * seq_per_img copies, dataloader.py:175, which it samples independently), row r reading image r / n and
+ * scored against its references; the rollout has B * n rows ([count, 2, B * n, seq_length] tokens). The
+ * greedy modes decode one row per image (their copies are identical) and so does the self-critical
+ * baseline. Default 1 (a caller may instead pass the copies as rows of the batch). */
+int nicnes_set_rows_per_image(nicnes_handle* h, int32_t n);
+
 /* Draws of the sampled modes (not a reference interface; the test hook that replays the reference's
  * numpy draws): the uniforms the next sampled evaluates use, u_host [count, 2, B, seq_length] fp64 (member,
  * sign, row, logit step), copied; n = 0 returns to the engine's own draws (a counter-based hash of the

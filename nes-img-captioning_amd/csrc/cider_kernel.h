@@ -37,14 +37,15 @@ extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int
 // lp (nullable) [n_cand, B, T] per-step log-probs; crit = fitness criterion (nicnes_set_fitness_mode)
 // scores: scratch [n_cand, B] fp64 (per-row CIDEr-D, reduced by a second kernel)
 // member_batch (nullable) [n_cand / 2]: candidate c scores against images member_batch[c / 2] * B + b.
-// crit: nicnes.h NICNES_FITNESS_*; base (nullable, crit 6 / 7) [n_cand, B]: the greedy rows' scores the
-// self-critical modes subtract. scores ([n_cand, B]) receives every row's CIDEr-D (cider_img: always,
-// as scratch; cider: when non-null)
+// crit: nicnes.h NICNES_FITNESS_*. B = rows per candidate, rpi of them per image (row b scores against image
+// b / rpi: the sampled modes' seq_per_img copies). base (nullable, crit 6 / 7) [n_cand, B / rpi]: the greedy
+// rows' scores (one per image) the self-critical modes subtract. scores ([n_cand, B]) receives every row's
+// CIDEr-D (cider_img: always, as scratch; cider: when non-null)
 extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
                                               const int32_t* img_ref_start, const int32_t* member_batch, const float* lp,
                                               int crit, double* scores, double* fitness_out, hipStream_t stream,
-                                              const double* base = nullptr);
+                                              const double* base = nullptr, int rpi = 1);
 extern "C" hipError_t nicnes_launch_cider(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
                                           const int32_t* img_ref_start, const int32_t* member_batch, const float* lp,
                                           int crit, double* fitness_out, hipStream_t stream, const double* base = nullptr,
-                                          double* scores = nullptr);
+                                          double* scores = nullptr, int rpi = 1);

@@ -156,11 +156,11 @@ __global__ __launch_bounds__(256) void nicnes_cook_refs_kernel(const int32_t* re
 // scores. crit 7 ('sc_loss'): LogFitnessCriterion (fitness.py:12-40), -lp * reward * mask with reward =
 // the row's self-critical score difference (policies.py:119-123, get_criterium :50-52).
 __device__ void finish_fitness(const double* row_score, const int32_t* seq, const float* lp, int B, int T, int crit,
-                               double* out, const double* base = nullptr) {
+                               double* out, const double* base = nullptr, int base_rpi = 1) {
     if (crit == 0 || crit == 5 || crit == 6 || lp == nullptr) {
         if (threadIdx.x == 0) {
             double s = 0.0;
-            for (int b = 0; b < B; ++b) s += row_score[b] - (crit == 6 && base ? base[b] : 0.0);
+            for (int b = 0; b < B; ++b) s += row_score[b] - (crit == 6 && base ? base[b / base_rpi] : 0.0);
             *out = (s / (double)B) * 100.0;
         }
         return;
@@ -169,7 +169,7 @@ __device__ void finish_fitness(const double* row_score, const int32_t* seq, cons
     double num = 0.0, den = 0.0;
     const float third = (float)(1.0 / 9.0), l9 = (float)0.9542425094393249, em1 = (float)(2.718281828459045 - 1.0);
     for (int b = threadIdx.x; b < B; b += blockDim.x) {
-        const float reward = (float)(row_score[b] - (base ? base[b] : 0.0));
+        const float reward = (float)(row_score[b] - (base ? base[b / base_rpi] : 0.0));
         for (int t = 0; t < T; ++t) {
             if (t > 0 && seq[(size_t)b * T + t - 1] <= 0) break;   // masked from here on
             const float p = expf(lp[(size_t)b * T + t]);
@@ -202,11 +202,11 @@ __device__ void finish_fitness(const double* row_score, const int32_t* seq, cons
 __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, int B, int T, CiderTables tb,
                                                            const int32_t* img_ref_start, const int32_t* member_batch,
                                                            const float* lp, int crit, double* fitness_out,
-                                                           const double* base, double* scores_out) {
+                                                           const double* base, double* scores_out, int rpi) {
     __shared__ double row_score[1024];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int cand = blockIdx.x;
-    img_ref_start += member_batch ? member_batch[cand >> 1] * B : 0;     // this member's batch (single_batch: false)
+    img_ref_start += member_batch ? member_batch[cand >> 1] * (B / rpi) : 0;   // this member's batch (single_batch: false)
     const double sigma2x2 = 2.0 * 6.0 * 6.0;
     for (int b = wave; b < B; b += 4) {
         const int32_t* row = seq + ((size_t)cand * B + b) * T;
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, i
         const int L = caption_len(row, T);
         const int len_h = L > 1 ? L - 1 : 0;
         double score = 0.0;                                                  // score[n] of this segment
-        const int r0 = img_ref_start[b], r1 = img_ref_start[b + 1];
+        const int r0 = img_ref_start[b / rpi], r1 = img_ref_start[b / rpi + 1];   // row b's image
         for (int r = r0; r < r1; ++r) {
             // vr[g] for this lane's n-gram (0 when the ref lacks it)
             const int cnt = tb.ref_count[r];
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, i
     if (scores_out)
         for (int b = threadIdx.x; b < B; b += blockDim.x) scores_out[(size_t)cand * B + b] = row_score[b];
     finish_fitness(row_score, seq + (size_t)cand * B * T, lp ? lp + (size_t)cand * B * T : nullptr, B, T, crit,
-                   fitness_out + cand, base ? base + (size_t)cand * B : nullptr);
+                   fitness_out + cand, base ? base + (size_t)cand * (B / rpi) : nullptr, rpi);
 }
 
 extern "C" uint64_t nicnes_df_hash_capacity(int64_t n) {
@@ -273,10 +273,10 @@ extern "C" hipError_t nicnes_launch_cook_refs(const int32_t* ref_tokens, int n_r
 extern "C" hipError_t nicnes_launch_cider(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
                                           const int32_t* img_ref_start, const int32_t* member_batch, const float* lp,
                                           int crit, double* fitness_out, hipStream_t stream, const double* base,
-                                          double* scores_out) {
-    if (B > 1024) return hipErrorInvalidValue;
+                                          double* scores_out, int rpi) {
+    if (B > 1024 || rpi < 1 || B % rpi) return hipErrorInvalidValue;
     hipLaunchKernelGGL(nicnes_cider_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, *tb, img_ref_start,
-                       member_batch, lp, crit, fitness_out, base, scores_out);
+                       member_batch, lp, crit, fitness_out, base, scores_out, rpi);
     return hipGetLastError();
 }
 
@@ -328,10 +328,10 @@ __global__ __launch_bounds__(64) void nicnes_img_ngram_kernel(const int32_t* img
 #define CIDER_IMG_ROWS 32
 __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* seq, int B, int T, CiderTables tb,
                                                                const int32_t* img_ref_start, const int32_t* member_batch,
-                                                               double* scores) {
+                                                               double* scores, int rpi) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int cand = blockIdx.x;
-    const int img0 = member_batch ? member_batch[cand >> 1] * B : 0;      // this member's batch (single_batch: false)
+    const int img0 = member_batch ? member_batch[cand >> 1] * (B / rpi) : 0;   // this member's batch (single_batch: false)
     const int b_end = min(B, (int)(blockIdx.y + 1) * CIDER_IMG_ROWS);
     const double sigma2x2 = 2.0 * 6.0 * 6.0;
     for (int b = (int)blockIdx.y * CIDER_IMG_ROWS + wave; b < b_end; b += 4) {
@@ -340,19 +340,20 @@ __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* se
         const double nh = sqrt(seg_sum(g.first ? g.vec * g.vec : 0.0));
         const int L = caption_len(row, T);
         const int len_h = L > 1 ? L - 1 : 0;
+        const int im = img0 + b / rpi;                                     // row b's image
         int trow = -1;
         if (g.first) {
             uint32_t slot = (uint32_t)df_hash(g.key) & (IMG_CAP - 1);
             for (int probe = 0; probe < IMG_CAP; ++probe) {
-                const uint64_t k = tb.img_hkey[(size_t)(img0 + b) * IMG_CAP + slot];
-                if (k == g.key) { trow = tb.img_hrow[(size_t)(img0 + b) * IMG_CAP + slot]; break; }
+                const uint64_t k = tb.img_hkey[(size_t)im * IMG_CAP + slot];
+                if (k == g.key) { trow = tb.img_hrow[(size_t)im * IMG_CAP + slot]; break; }
                 if (k == 0ull) break;
                 slot = (slot + 1) & (IMG_CAP - 1);
             }
         }
-        const double* vrow = tb.img_vr + ((size_t)(img0 + b) * IMG_ROWS + (trow >= 0 ? trow : 0)) * IMG_MAXR;
+        const double* vrow = tb.img_vr + ((size_t)im * IMG_ROWS + (trow >= 0 ? trow : 0)) * IMG_MAXR;
         double score = 0.0;
-        const int r0 = img_ref_start[img0 + b], r1 = img_ref_start[img0 + b + 1];
+        const int r0 = img_ref_start[im], r1 = img_ref_start[im + 1];
         for (int r = r0; r < r1; ++r) {
             const double vr = trow >= 0 ? vrow[r - r0] : 0.0;
             const double contrib = g.first ? (g.vec < vr ? g.vec : vr) * vr : 0.0;
@@ -376,10 +377,10 @@ __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* se
 
 __global__ __launch_bounds__(256) void nicnes_cider_finish_kernel(const int32_t* seq, int B, int T,
                                                                   const double* scores, const float* lp, int crit,
-                                                                  double* fitness_out, const double* base) {
+                                                                  double* fitness_out, const double* base, int rpi) {
     const int cand = blockIdx.x;
     finish_fitness(scores + (size_t)cand * B, seq + (size_t)cand * B * T, lp ? lp + (size_t)cand * B * T : nullptr,
-                   B, T, crit, fitness_out + cand, base ? base + (size_t)cand * B : nullptr);
+                   B, T, crit, fitness_out + cand, base ? base + (size_t)cand * (B / rpi) : nullptr, rpi);
 }
 
 extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int B, const CiderTables* tb,
@@ -391,11 +392,11 @@ extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int
 extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, int B, int T, const CiderTables* tb,
                                               const int32_t* img_ref_start, const int32_t* member_batch, const float* lp,
                                               int crit, double* scores, double* fitness_out, hipStream_t stream,
-                                              const double* base) {
-    if (B > 1024 || n_cand < 1) return hipErrorInvalidValue;
+                                              const double* base, int rpi) {
+    if (B > 1024 || n_cand < 1 || rpi < 1 || B % rpi) return hipErrorInvalidValue;
     hipLaunchKernelGGL(nicnes_cider_img_kernel, dim3(n_cand, (B + CIDER_IMG_ROWS - 1) / CIDER_IMG_ROWS), dim3(256), 0,
-                       stream, seq, B, T, *tb, img_ref_start, member_batch, scores);
+                       stream, seq, B, T, *tb, img_ref_start, member_batch, scores, rpi);
     hipLaunchKernelGGL(nicnes_cider_finish_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, (const double*)scores,
-                       lp, crit, fitness_out, base);
+                       lp, crit, fitness_out, base, rpi);
     return hipGetLastError();
 }

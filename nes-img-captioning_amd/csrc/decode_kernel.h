@@ -30,8 +30,10 @@ struct DecodeParams {
     int32_t bounded_lse;         // 1: greedy-only decode with the pair-bounded lse (needs lp == NULL)
     int32_t B, F, V1, T;         // B: rows decoded per sign and slab range
     int32_t B_img;               // images per batch in fc / the member_batch stride (= B, or the whole batch below)
-    int32_t sign_off;            // 0; > 0 (the sigma = 0 rollout decoded once): sign s decodes images s * sign_off + b,
-                                 // b < B, valid while < B_img, and its rows land at s * B + b of one [2B, T] rollout
+    int32_t sign_off;            // 0; > 0 (the sigma = 0 rollout decoded once): sign s decodes rows s * sign_off + b,
+                                 // b < B, valid while < B_img * rpi, and its rows land at s * B + b of one [2B, T] rollout
+    int32_t rpi;                 // rows per image (sampled modes: the reference's seq_per_img copies): row r reads
+                                 // fc row r / rpi
     int32_t G;                   // row groups per slab: 4 (128-row slabs) or 2 (64-row slabs)
     int32_t S;                   // logit workgroups per member slab (1 + G = 4: the fused step kernel)
     int32_t alive_stride;

@@ -929,10 +929,10 @@ struct Ctx {
     rsrc_t theta_r, noise_r, scr_r;
 };
 
-// a row is decoded when it lies in the slab range and its image in the batch (sign_off > 0: sign 1 takes the
-// second half of the images, DecodeParams::sign_off)
+// a row is decoded when it lies in the slab range and in the batch's B_img * rpi rows (sign_off > 0: sign 1 takes
+// the second half of the rows, DecodeParams::sign_off)
 __device__ __forceinline__ bool row_ok(const DecodeParams& p, int b, int sgn) {
-    return b < p.B && b + sgn * p.sign_off < p.B_img;
+    return b < p.B && b + sgn * p.sign_off < p.B_img * p.rpi;
 }
 
 __device__ __forceinline__ Ctx make_ctx(const DecodeParams& p) {
@@ -1008,7 +1008,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
     if (fused_path) PROF_MARK(80); else PROF_SPLIT(250);
     const float* fcm = p.fc + (p.member_batch ? (size_t)p.member_batch[c.member] * p.B_img * p.F : 0);
     const rsrc_t fc_r = make_rsrc(fcm, 4u * (uint32_t)p.B_img * (uint32_t)p.F);
-    const int fr = c.row_valid ? c.b + c.sgn * p.sign_off : 0;      // the lane's fc row
+    const int fr = c.row_valid ? (c.b + c.sgn * p.sign_off) / p.rpi : 0;      // the lane's fc row (its image)
     const uint32_t lo = 4u * c.lane;
     const bool mm = G == 4 || c.hf == 0;
     StageRegs sr;
@@ -1067,7 +1067,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img64_kernel(DecodePar
     PROF_MARK(80);
     const float* fcm = p.fc + (p.member_batch ? (size_t)p.member_batch[c.member] * p.B_img * p.F : 0);
     const rsrc_t fc_r = make_rsrc(fcm, 4u * (uint32_t)p.B_img * (uint32_t)p.F);
-    const int fr = c.row_valid ? c.b + c.sgn * p.sign_off : 0;      // the lane's fc row
+    const int fr = c.row_valid ? (c.b + c.sgn * p.sign_off) / p.rpi : 0;      // the lane's fc row (its image)
     const int nK = p.F >> 7;
     const uint32_t F = (uint32_t)p.F;
     auto load = [&](int j, Stage64Regs& r) __attribute__((always_inline)) {

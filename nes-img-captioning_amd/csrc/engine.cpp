@@ -86,6 +86,7 @@ struct nicnes_handle {
     double* base_scores = nullptr;    // self-critical modes: the greedy rows' CIDEr-D [2 count, B]
     int64_t su_cap = 0, base_cap = 0; // ... their capacities (doubles)
     std::vector<double> su_host;      // nicnes_set_sample_draws (test hook): draws to use instead of the engine's
+    int rpi = 1;                      // nicnes_set_rows_per_image: rows the sampled modes decode per image
     float* dscratch = nullptr;
     int32_t* stats = nullptr;
     int32_t* alive = nullptr;         // per decode workgroup: rows left unfinished (fused [stride], split [2][stride])
@@ -638,6 +639,12 @@ int nicnes_set_mutation(nicnes_handle* h, int32_t mode, const float* vec, void* 
     return NICNES_OK;
 }
 
+int nicnes_set_rows_per_image(nicnes_handle* h, int32_t n) {
+    if (!h || n < 1 || n > 64) return NICNES_ERR_INVALID;
+    h->rpi = n;
+    return NICNES_OK;
+}
+
 int nicnes_set_sample_draws(nicnes_handle* h, const double* u_host, int64_t n) {
     if (!h || n < 0 || (n > 0 && !u_host)) return NICNES_ERR_INVALID;
     h->su_host.assign(u_host, u_host + n);
@@ -792,8 +799,16 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     bool bounded = h->bounded_mode == 1 || (h->bounded_mode == 2 && h->exact_left == 0);
     if (h->bounded_mode == 2 && h->exact_left > 0 && !p.lp) --h->exact_left;
     p.bounded_lse = bounded ? 1 : 0;
-    // rows per sign: the batch, or its first half (eval_theta; sign - takes images half + b)
-    const int rows = eval_theta ? (h->B + 1) / 2 : h->B;
+    // rollout rows: the images, or rpi copies of each in the sampled modes (the reference's seq_per_img rows);
+    // rows per sign: all of them, or the first half (eval_theta; sign - takes rows half + b)
+    const int rpi = sampled ? h->rpi : 1;
+    const int rows_total = h->B * rpi;
+    const int rows = eval_theta ? (rows_total + 1) / 2 : rows_total;
+    if (rows_total > h->cfg.max_batch) {      // rpi copies outgrow the row buffers
+        HIPC(h, hipDeviceSynchronize());
+        int rc = alloc_batch(h, rows_total);
+        if (rc) return rc;
+    }
     int G = 0, nslabs = 0, S = 0;
     decode_shape(h, rows, count, &G, &nslabs, &S);
     if (sampled) {          // the sampled pick runs on the fused path (128-row slabs, one workgroup per slab)
@@ -835,6 +850,7 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     p.alive_stride = h->alive_stride;
     p.B = rows;
     p.B_img = h->B;
+    p.rpi = rpi;
     p.sign_off = eval_theta ? rows : 0;
     p.F = h->cfg.fc_feat_size;
     p.V1 = h->V1;
@@ -884,7 +900,7 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     h->n_dev = h->timing ? n_ev : 0;
     h->multi_stream = nstr > 1;
     if (p.no_exit)      // eval_theta: the two halves are one rollout
-        HIPC(h, nicnes_launch_lp_batch_exit(p.seq, p.lp, eval_theta ? 1 : 2 * count, eval_theta ? 2 * rows : h->B,
+        HIPC(h, nicnes_launch_lp_batch_exit(p.seq, p.lp, eval_theta ? 1 : 2 * count, eval_theta ? 2 * rows : rows_total,
                                             h->cfg.seq_length, s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     if (!h->stats_pending) {          // read the fallback counter back without a host wait
@@ -897,14 +913,14 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     const int n_cand = eval_theta ? 1 : 2 * count;      // eval_theta: rows s * half + b = image s * half + b
     const double* base = self_critical ? h->base_scores : nullptr;
     if (h->img_tables) {
-        HIPC(h, nicnes_launch_cider_img(p.seq, n_cand, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
-                                         h->fitness_mode, h->row_scores, fitness_out, s, base));
+        HIPC(h, nicnes_launch_cider_img(p.seq, n_cand, rows_total, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
+                                         h->fitness_mode, h->row_scores, fitness_out, s, base, rpi));
         if (scores_out)
-            HIPC(h, hipMemcpyAsync(scores_out, h->row_scores, (size_t)n_cand * h->B * sizeof(double),
+            HIPC(h, hipMemcpyAsync(scores_out, h->row_scores, (size_t)n_cand * rows_total * sizeof(double),
                                    hipMemcpyDeviceToDevice, s));
     } else {
-        HIPC(h, nicnes_launch_cider(p.seq, n_cand, h->B, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
-                                    h->fitness_mode, fitness_out, s, base, scores_out));
+        HIPC(h, nicnes_launch_cider(p.seq, n_cand, rows_total, h->cfg.seq_length, &tb, h->img_ref_start, mb, p.lp,
+                                    h->fitness_mode, fitness_out, s, base, scores_out, rpi));
     }
     if (h->timing) HIPC(h, hipEventRecord(h->ev[2], s));
     return NICNES_OK;
@@ -970,6 +986,7 @@ int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, floa
     p.no_mask = 1;
     p.B = rows;
     p.B_img = h->B;
+    p.rpi = 1;
     p.sign_off = 0;
     p.F = h->cfg.fc_feat_size;
     p.V1 = h->V1;

@@ -21,7 +21,7 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_comm_attach', 'nicnes_comm_destroy', 'nicnes_allgather_fitness', 'nicnes_allreduce_grad',
            'nicnes_noise_vectors', 'nicnes_set_batches', 'nicnes_evaluate_batches', 'nicnes_set_mutation',
            'nicnes_set_decode_coop', 'nicnes_decode_path', 'nicnes_sum_sensitivity', 'nicnes_grad_partial_range',
-           'nicnes_evaluate_theta', 'nicnes_set_sample_draws']
+           'nicnes_evaluate_theta', 'nicnes_set_sample_draws', 'nicnes_set_rows_per_image']
 
 
 class NicnesConfig(ctypes.Structure):
@@ -73,6 +73,7 @@ def lib(path=None):
         'nicnes_evaluate_batches': (c.c_int, [vp, u64, i32, i32, f32, vp, vp, vp, vp, vp]),
         'nicnes_evaluate_theta': (c.c_int, [vp, i32, vp, vp, vp, vp]),
         'nicnes_set_sample_draws': (c.c_int, [vp, vp, i64]),
+        'nicnes_set_rows_per_image': (c.c_int, [vp, i32]),
         'nicnes_rank_weights': (c.c_int, [vp, vp, i32, vp, vp, vp]),
         'nicnes_grad_partial': (c.c_int, [vp, u64, i32, i32, vp, f32, vp, vp]),
         'nicnes_grad_partial_range': (c.c_int, [vp, u64, i32, i32, vp, f32, i64, i64, vp, vp]),

@@ -62,6 +62,8 @@ class Engine:
         self.coop_mode = 0 if os.environ.get('NICNES_DECODE_COOP') == '0' else 1
         self._keep = {}
         self.B = 0
+        self.fitness_mode = 0
+        self.rpi = 1
 
     # -------------------------------------------------------------------------------------
     def close(self):
@@ -216,7 +218,7 @@ class Engine:
         index of its batch among set_batches' (None: the one batch held)."""
         fit = fitness_out if fitness_out is not None else torch.empty((count, 2), dtype=torch.float64,
                                                                       device=self.device)
-        shape = (count, 2, self.B, self.cfg.seq_length)
+        shape = (count, 2, self.rollout_rows(), self.cfg.seq_length)
         seq = torch.empty(shape, dtype=torch.int32, device=self.device) if return_seq else None
         lp = torch.empty(shape, dtype=torch.float32, device=self.device) if return_lp else None
         mb = None
@@ -231,6 +233,16 @@ class Engine:
                                                  self._stream()), self.h, 'evaluate')
         out = (fit,) + ((seq,) if return_seq else ()) + ((lp,) if return_lp else ())
         return out if len(out) > 1 else fit
+
+    def set_rows_per_image(self, n=1):
+        """Sampled modes: decode n rows per image of the batch (the reference's seq_per_img copies, each with
+        its own draws); greedy modes always decode one."""
+        check(self.L.nicnes_set_rows_per_image(self.h, int(n)), self.h, 'set_rows_per_image')
+        self.rpi = int(n)
+
+    def rollout_rows(self):
+        """Rows of one rollout: the batch's images, times rows_per_image in the sampled modes."""
+        return self.B * (getattr(self, 'rpi', 1) if self.fitness_mode in self.SAMPLED_MODES else 1)
 
     def set_sample_draws(self, u=None):
         """Test hook: the uniforms [count, 2, B, T] fp64 the next sampled evaluates use (None: the engine's
@@ -249,7 +261,7 @@ class Engine:
         rollout (CaptPolicy.rollout) decoded once, sign + over the first half of the images and sign -
         over the rest. Tensor [1] fp64 on the GPU; return_seq / return_lp add [B, T] tokens / log-probs."""
         fit = torch.empty(1, dtype=torch.float64, device=self.device)
-        shape = (self.B, self.cfg.seq_length)
+        shape = (self.rollout_rows(), self.cfg.seq_length)
         seq = torch.empty(shape, dtype=torch.int32, device=self.device) if return_seq else None
         lp = torch.empty(shape, dtype=torch.float32, device=self.device) if return_lp else None
         with torch.cuda.device(self.device):

@@ -80,24 +80,14 @@ def unique_batch(data, seq_per_img=5):
 SAMPLED_FITNESS_CODES = (5, 6, 7)     # 'sample', 'self_critical', 'sc_loss' (nicnes.h NICNES_FITNESS_*)
 
 
-def sampled_batch(data, seq_per_img=5):
-    """Reference batch dict -> (fc [B*seq_per_img, F], gts per row): every row the reference decodes.
-    Sampled decoding (FCModel._sample, greedy=False) draws each duplicated row independently, so the rows
-    are kept and row i scores against image i // seq_per_img (compute_ciders, policies.py:161-170)."""
-    fc = np.ascontiguousarray(np.asarray(data['fc_feats'], np.float32))
-    gts = data['gts']
-    spi = fc.shape[0] // len(gts)
-    if spi * len(gts) != fc.shape[0]:
-        raise ValueError('fc_feats rows (%d) are not a multiple of the %d images of gts' % (fc.shape[0], len(gts)))
-    return fc, [gts[i // spi] for i in range(fc.shape[0])]
-
-
 def engine_batch(data, engine, seq_per_img=5):
-    """The rows the engine decodes for its fitness mode: one per image for the greedy modes (unique_batch),
-    all of them for the sampled modes (sampled_batch)."""
-    if getattr(engine, 'fitness_mode', 0) in SAMPLED_FITNESS_CODES:
-        return sampled_batch(data, seq_per_img)
-    return unique_batch(data, seq_per_img)
+    """The images the engine holds for a reference batch dict (unique_batch). The sampled modes decode every
+    copy of an image, so the engine is told how many rows each image has (Engine.set_rows_per_image, the
+    batch's seq_per_img); the copies are not uploaded."""
+    fc, gts = unique_batch(data, seq_per_img)
+    if getattr(engine, 'fitness_mode', 0) in SAMPLED_FITNESS_CODES and hasattr(engine, 'set_rows_per_image'):
+        engine.set_rows_per_image(max(1, np.asarray(data['fc_feats']).shape[0] // len(gts)))
+    return fc, gts
 
 
 def member_batches(batch_data, member_begin, count):

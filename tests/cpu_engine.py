@@ -41,6 +41,9 @@ class OracleEngine:
         s = SR.sum_sensitivity((d.vocab_size + 1, d.E, d.R, d.F), self.theta32, fc[:rows], rows)
         return clamp_calc(s, underflow) if underflow > 0 else s
 
+    def set_rows_per_image(self, n=1):
+        self.rpi = int(n)
+
     def set_fitness_mode(self, fitness):
         self.fitness_mode = CR.CRITERIA[fitness] if isinstance(fitness, str) else int(fitness)
 

@@ -169,9 +169,10 @@ def test_engine_draws_are_deterministic_per_iteration(eng):
     assert len(np.unique(a[:, :, :, 0])) > 10                          # flat xavier logits: many first words
 
 
-def test_policy_keeps_duplicated_rows_for_sampled_modes(eng):
-    """EnginePolicy.rollout with 'sample': the 5 duplicated rows of each image are decoded (each draws its
-    own tokens, dataloader.py:175), greedy modes decode one row per image."""
+def test_policy_decodes_every_copy_for_sampled_modes(eng):
+    """EnginePolicy.rollout with 'sample': the 5 copies of each image (dataloader.py:175) are decoded, each
+    drawing its own tokens (rows_per_image 5 over the 8 unique images held); greedy modes decode one row per
+    image."""
     import nicnes.nes as N
     dims = O.Dims()
     theta = O.make_theta(dims, 0, 1.0, 0.0)
@@ -182,12 +183,46 @@ def test_policy_keeps_duplicated_rows_for_sampled_modes(eng):
     eng.set_fitness_mode('sample')
     try:
         f = pol.rollout(None, data, None)
-        assert eng.B == 40 and np.isfinite(f)
+        assert eng.B == 8 and eng.rpi == 5 and eng.rollout_rows() == 40 and np.isfinite(f)
+        _, seq = eng.evaluate(2, 0, 1, SIGMA, return_seq=True)
+        seq = seq.cpu().numpy()
+        assert seq.shape == (1, 2, 40, dims.T)
+        assert any(not np.array_equal(seq[0, 0, 5 * i], seq[0, 0, 5 * i + 1]) for i in range(8))
     finally:
         eng.set_fitness_mode('greedy')
-    pol._batch_key = None
-    pol.rollout(None, data, None)
-    assert eng.B == 8
+        eng.set_rows_per_image(1)
+    assert eng.rollout_rows() == 8
+
+
+def test_rows_per_image_equals_duplicated_rows(eng):
+    """rows_per_image 5 over B unique images = the same batch passed as its 5 B duplicated rows (rows_per_image
+    1), with the same draws: tokens, log-probs and fitness identical, for every sampled mode (the self-critical
+    baseline then decodes B rows instead of 5 B)."""
+    dims = O.Dims()
+    theta = O.make_theta(dims, 0, 4.0, 0.1)
+    B = 12
+    fc = np.random.Generator(np.random.PCG64(21)).standard_normal((B, dims.F)).astype(np.float32)
+    gts, _ = _load(eng, theta, fc)
+    u = np.random.Generator(np.random.PCG64(22)).random((2, 2, 5 * B, dims.T))
+    res = {}
+    try:
+        eng.set_sample_draws(u)
+        for mode in ('sample', 'self_critical', 'sc_loss'):
+            eng.set_fitness_mode(mode)
+            eng.set_batch(fc, gts)
+            eng.set_rows_per_image(5)
+            a = [x.cpu().numpy() for x in eng.evaluate(7, 0, 2, SIGMA, return_seq=True, return_lp=True)]
+            eng.set_rows_per_image(1)
+            eng.set_batch(np.repeat(fc, 5, 0), [g for g in gts for _ in range(5)])
+            b = [x.cpu().numpy() for x in eng.evaluate(7, 0, 2, SIGMA, return_seq=True, return_lp=True)]
+            res[mode] = (a, b)
+    finally:
+        eng.set_sample_draws(None)
+        eng.set_rows_per_image(1)
+        eng.set_fitness_mode('greedy')
+    for mode, (a, b) in res.items():
+        assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]), mode
+        assert np.allclose(a[0], b[0], rtol=1e-12, atol=1e-12), (mode, a[0], b[0])
 
 
 def test_sampled_with_member_batches_and_mutation(eng):
