@@ -679,16 +679,14 @@ __device__ __forceinline__ void exact_sweep(float* lds, const DecodeParams& p, r
 
 // One sweep of the vocabulary in 32-row tiles for the sampled pick (FCModel._sample with greedy=False,
 // nets.py:210-231; RandomState.choice: the first id whose cumulative probability exceeds the draw): the
-// row's cumulative sum of e^(x - m) in index order, in fp64, against thr = u * the logit loop's exp-sum. Each
-// term is formed exactly as the logit loop formed its exp-sum terms (exp2(x log2e - ml), ml = fp32(m log2e)),
-// so the two sums share their rounding of m log2e and agree to the loop's rescalings (~1e-7). A lane
+// row's cumulative sum of p = exp((x - m) - lse) in index order, in fp64, against thr = u * sum(p). A lane
 // holds ids 32n + 8k + 4hh + e (k, e < 4): per tile the two lanes of a row exchange their four group sums
 // and walk the eight groups in id order; the lane holding the crossing group walks its four ids. tok /
 // lpv: the pick and its log-prob (logprobs.gather, nets.py:225); V1 - 1 if the sums never reach thr.
-__device__ __forceinline__ void sample_sweep(float* lds, const DecodeParams& p, rsrc_t theta_r, rsrc_t noise_r,
-                                             int tid, int sgn, int hh, int lane, const float (&hB)[64], float m,
-                                             float lse, double thr, int& tok, float& lpv) {
-    const float ml = m * LOG2E;
+// Returns the row's total of p in the same order (thr = +inf: the total alone).
+__device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p, rsrc_t theta_r, rsrc_t noise_r,
+                                               int tid, int sgn, int hh, int lane, const float (&hB)[64], float m,
+                                               float lse, double thr, int& tok, float& lpv) {
     const int nvt = (p.V1 + 31) >> 5;
     auto desc = [&](int n) {
         TileDesc d;
@@ -716,8 +714,9 @@ __device__ __forceinline__ void sample_sweep(float* lds, const DecodeParams& p, 
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int v = vb + 8 * k + e;
-                g[k] += v < p.V1 ? (double)__builtin_amdgcn_exp2f(__builtin_fmaf(acc[4 * k + e], LOG2E, -ml)) : 0.0;
-                if (v == p.V1 - 1) lastlp = (acc[4 * k + e] - m) - lse;
+                const float x = (acc[4 * k + e] - m) - lse;
+                g[k] += v < p.V1 ? (double)nn_expf(x) : 0.0;
+                if (v == p.V1 - 1) lastlp = x;
             }
         }
         double go[4];
@@ -737,9 +736,9 @@ __device__ __forceinline__ void sample_sweep(float* lds, const DecodeParams& p, 
                     bool hit = false;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        c2 += vb + 8 * k + e < p.V1
-                                  ? (double)__builtin_amdgcn_exp2f(__builtin_fmaf(acc[4 * k + e], LOG2E, -ml)) : 0.0;
-                        if (!hit && c2 > thr) { hit = true; pick = vb + 8 * k + e; plp = (acc[4 * k + e] - m) - lse; }
+                        const float x = (acc[4 * k + e] - m) - lse;
+                        c2 += vb + 8 * k + e < p.V1 ? (double)nn_expf(x) : 0.0;
+                        if (!hit && c2 > thr) { hit = true; pick = vb + 8 * k + e; plp = x; }
                     }
                     mine = min(pick, p.V1 - 1);
                     mlp = plp;
@@ -755,6 +754,7 @@ __device__ __forceinline__ void sample_sweep(float* lds, const DecodeParams& p, 
     if (mine != 0x7fffffff) { tok = mine; lpv = mlp; }
     else if (other != 0x7fffffff) { tok = other; lpv = olp; }
     else { tok = p.V1 - 1; lpv = ((p.V1 - 1) & 4) >> 2 == hh ? lastlp : olast; }
+    return cum;
 }
 
 // epilogue of one 32-row logit tile (G = 2: one tile per wave); P0 holds vocab vbase + (r&3) + 8(r>>2)
@@ -1229,9 +1229,11 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         if constexpr (SAMPLE) {
             const size_t ou = (((size_t)c.member * 2 + c.sgn) * p.B + c.bc) * p.T + (t - 1);
             const double u = c.row_valid ? p.sample_u[ou] : 0.5;
-            // thr = u * the row's exp-sum (relative to m), summed by the logit loop with the terms the sweep forms
-            sample_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, u * (double)stot, tok,
-                         lp_tok);
+            // thr = u * the row's sum of p, summed by a first sweep exactly as the walk sums (the pass-1 exp-sum
+            // differs from it by ~1e-6: its exponents carry the rounding of m * log2e)
+            const double tot = sample_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, m, lse,
+                                            __builtin_inf(), tok, lp_tok);
+            sample_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, u * tot, tok, lp_tok);
         } else {
             const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
             const int ci[4] = {st.r0i, st.r1i, __shfl_xor(st.r0i, 32), __shfl_xor(st.r1i, 32)};
