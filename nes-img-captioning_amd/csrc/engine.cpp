@@ -719,6 +719,15 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     if (!h->batch_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_batch first");
     hipStream_t s = (hipStream_t)stream;
     HIPC(h, hipSetDevice(h->device));
+    // rollout rows: the images, or rpi copies of each in the sampled modes (the reference's seq_per_img rows);
+    // the row buffers grow before anything below takes their addresses
+    const int rpi = sampled ? h->rpi : 1;
+    const int rows_total = h->B * rpi;
+    if (rows_total > h->cfg.max_batch) {
+        HIPC(h, hipDeviceSynchronize());
+        int rc = alloc_batch(h, rows_total);
+        if (rc) return rc;
+    }
     const int32_t* mb = nullptr;
     if (member_batch_host) {
         for (int k = 0; k < count; ++k)
@@ -799,16 +808,8 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     bool bounded = h->bounded_mode == 1 || (h->bounded_mode == 2 && h->exact_left == 0);
     if (h->bounded_mode == 2 && h->exact_left > 0 && !p.lp) --h->exact_left;
     p.bounded_lse = bounded ? 1 : 0;
-    // rollout rows: the images, or rpi copies of each in the sampled modes (the reference's seq_per_img rows);
-    // rows per sign: all of them, or the first half (eval_theta; sign - takes rows half + b)
-    const int rpi = sampled ? h->rpi : 1;
-    const int rows_total = h->B * rpi;
+    // rows per sign: all of the rollout's rows, or the first half (eval_theta; sign - takes rows half + b)
     const int rows = eval_theta ? (rows_total + 1) / 2 : rows_total;
-    if (rows_total > h->cfg.max_batch) {      // rpi copies outgrow the row buffers
-        HIPC(h, hipDeviceSynchronize());
-        int rc = alloc_batch(h, rows_total);
-        if (rc) return rc;
-    }
     int G = 0, nslabs = 0, S = 0;
     decode_shape(h, rows, count, &G, &nslabs, &S);
     if (sampled) {          // the sampled pick runs on the fused path (128-row slabs, one workgroup per slab)

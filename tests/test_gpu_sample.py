@@ -200,7 +200,7 @@ def test_rows_per_image_equals_duplicated_rows(eng):
     baseline then decodes B rows instead of 5 B)."""
     dims = O.Dims()
     theta = O.make_theta(dims, 0, 4.0, 0.1)
-    B = 12
+    B = 30                                                  # 150 rows: past max_batch (128) and two slabs
     fc = np.random.Generator(np.random.PCG64(21)).standard_normal((B, dims.F)).astype(np.float32)
     gts, _ = _load(eng, theta, fc)
     u = np.random.Generator(np.random.PCG64(22)).random((2, 2, 5 * B, dims.T))
