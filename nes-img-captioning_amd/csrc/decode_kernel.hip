@@ -677,85 +677,6 @@ __device__ __forceinline__ void exact_sweep(float* lds, const DecodeParams& p, r
     }
 }
 
-// One sweep of the vocabulary in 32-row tiles for the sampled pick (FCModel._sample with greedy=False,
-// nets.py:210-231; RandomState.choice: the first id whose cumulative probability exceeds the draw): the
-// row's cumulative sum of p = exp((x - m) - lse) in index order, in fp64, against thr = u * sum(p). A lane
-// holds ids 32n + 8k + 4hh + e (k, e < 4): per tile the two lanes of a row exchange their four group sums
-// and walk the eight groups in id order; the lane holding the crossing group walks its four ids. tok /
-// lpv: the pick and its log-prob (logprobs.gather, nets.py:225); V1 - 1 if the sums never reach thr.
-// Returns the row's total of p in the same order (thr = +inf: the total alone).
-__device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p, rsrc_t theta_r, rsrc_t noise_r,
-                                               int tid, int sgn, int hh, int lane, const float (&hB)[64], float m,
-                                               float lse, double thr, int& tok, float& lpv) {
-    const int nvt = (p.V1 + 31) >> 5;
-    auto desc = [&](int n) {
-        TileDesc d;
-        d.w_off = (uint32_t)p.off_log_w; d.ld = 128; d.row0 = 32 * n; d.nvalid = min(32, p.V1 - 32 * n); d.k0 = 0;
-        d.b_off = (uint32_t)p.off_log_b; d.pad_bias = NEG_INF;
-        return d;
-    };
-    StageRegs sr;
-    stage_load(theta_r, noise_r, desc(0), tid, sr);
-    stage_store(lds, desc(0), tid, sr);
-    __syncthreads();
-    double cum = 0.0;
-    bool found = false;
-    int mine = 0x7fffffff;
-    float mlp = 0.f, lastlp = 0.f;
-    for (int n = 0; n < nvt; ++n) {
-        if (n + 1 < nvt) stage_load(theta_r, noise_r, desc(n + 1), tid, sr);
-        const float* buf = lds + (n & 1) * STAGE_FLOATS;
-        const f32x16 acc = mfma_tile(bias_init(buf + 2 * SIGN_FLOATS + 32 * sgn, hh), buf + sgn * SIGN_FLOATS, hB, lane);
-        const int vb = 32 * n + 4 * hh;
-        double g[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            g[k] = 0.0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int v = vb + 8 * k + e;
-                const float x = (acc[4 * k + e] - m) - lse;
-                g[k] += v < p.V1 ? (double)nn_expf(x) : 0.0;
-                if (v == p.V1 - 1) lastlp = x;
-            }
-        }
-        double go[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) go[k] = __shfl_xor(g[k], 32);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {                    // groups in id order: (k, half) = (j >> 1, j & 1)
-            const int k = j >> 1;
-            const bool own = (j & 1) == hh;
-            const double gs = own ? g[k] : go[k];
-            if (!found && cum + gs > thr) {
-                found = true;
-                if (own) {
-                    double c2 = cum;
-                    int pick = vb + 8 * k + 3;
-                    float plp = (acc[4 * k + 3] - m) - lse;
-                    bool hit = false;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const float x = (acc[4 * k + e] - m) - lse;
-                        c2 += vb + 8 * k + e < p.V1 ? (double)nn_expf(x) : 0.0;
-                        if (!hit && c2 > thr) { hit = true; pick = vb + 8 * k + e; plp = x; }
-                    }
-                    mine = min(pick, p.V1 - 1);
-                    mlp = plp;
-                }
-            }
-            if (!found) cum += gs;
-        }
-        if (n + 1 < nvt) stage_store(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), tid, sr);
-        __syncthreads();
-    }
-    const int other = __shfl_xor(mine, 32);
-    const float olp = __shfl_xor(mlp, 32), olast = __shfl_xor(lastlp, 32);
-    if (mine != 0x7fffffff) { tok = mine; lpv = mlp; }
-    else if (other != 0x7fffffff) { tok = other; lpv = olp; }
-    else { tok = p.V1 - 1; lpv = ((p.V1 - 1) & 4) >> 2 == hh ? lastlp : olast; }
-    return cum;
-}
 
 // epilogue of one 32-row logit tile (G = 2: one tile per wave); P0 holds vocab vbase + (r&3) + 8(r>>2)
 template <bool PAIRS>
@@ -809,6 +730,84 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
     Sx.bso = 256u * (uint32_t)s; Sx.bda = 0u; Sx.bdb = 128u;
     Sx.valid = p.V1 - 64 * s;
     return Sx;
+}
+
+// One sweep of the vocabulary in 64-row stages for the sampled pick (FCModel._sample with greedy=False,
+// nets.py:210-231; RandomState.choice: the first id whose cumulative probability exceeds the draw): the
+// row's cumulative sum of p = exp((x - m) - lse) in index order, in fp64, against thr = u * sum(p). The
+// stages are the logit loop's (two MFMA chains per wave, staged through r); a lane holds, per chain c,
+// ids 64s + 32c + 8k + 4hh + e (k, e < 4): the two lanes of a row exchange their four group sums and walk
+// the eight groups of each chain in id order; the lane holding the crossing group walks its four ids. tok /
+// lpv: the pick and its log-prob (logprobs.gather, nets.py:225); V1 - 1 if the sums never reach thr.
+// Returns the row's total of p in the same order (thr = +inf: the total alone).
+__device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p, uint64_t nidx, int tid, int sgn,
+                                               int hh, int lane, const float (&hB)[64], float m, float lse, double thr,
+                                               Stage64Regs& r, int& tok, float& lpv) {
+    const int nst = (p.V1 + 63) >> 6;
+    stage64_load(logit_src(p, nidx, 0), tid, r);
+    stage64_store(lds, logit_src(p, nidx, 0).valid, tid, r);
+    __syncthreads();
+    double cum = 0.0;
+    bool found = false;
+    int mine = 0x7fffffff;
+    float mlp = 0.f, lastlp = 0.f;
+    auto walk = [&](const f32x16& acc, int vb) __attribute__((always_inline)) {
+        double g[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            g[k] = 0.0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int v = vb + 8 * k + e;
+                const float x = (acc[4 * k + e] - m) - lse;
+                g[k] += v < p.V1 ? (double)nn_expf(x) : 0.0;
+                if (v == p.V1 - 1) lastlp = x;
+            }
+        }
+        double go[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) go[k] = __shfl_xor(g[k], 32);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {                    // groups in id order: (k, half) = (j >> 1, j & 1)
+            const int k = j >> 1;
+            const bool own = (j & 1) == hh;
+            const double gs = own ? g[k] : go[k];
+            if (!found && cum + gs > thr) {
+                found = true;
+                if (own) {
+                    double c2 = cum;
+                    int pick = vb + 8 * k + 3;
+                    float plp = (acc[4 * k + 3] - m) - lse;
+                    bool hit = false;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float x = (acc[4 * k + e] - m) - lse;
+                        c2 += vb + 8 * k + e < p.V1 ? (double)nn_expf(x) : 0.0;
+                        if (!hit && c2 > thr) { hit = true; pick = vb + 8 * k + e; plp = x; }
+                    }
+                    mine = min(pick, p.V1 - 1);
+                    mlp = plp;
+                }
+            }
+            if (!found) cum += gs;
+        }
+    };
+    for (int s = 0; s < nst; ++s) {
+        if (s + 1 < nst) stage64_load(logit_src(p, nidx, s + 1), tid, r);
+        const float* buf = lds + (s & 1) * STAGE64_FLOATS;
+        f32x16 a0, a1;
+        mfma_stage64(buf + sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * sgn, hB, lane, a0, a1);
+        walk(a0, 64 * s + 4 * hh);
+        walk(a1, 64 * s + 32 + 4 * hh);
+        if (s + 1 < nst) stage64_store(lds + ((s + 1) & 1) * STAGE64_FLOATS, logit_src(p, nidx, s + 1).valid, tid, r);
+        __syncthreads();
+    }
+    const int other = __shfl_xor(mine, 32);
+    const float olp = __shfl_xor(mlp, 32), olast = __shfl_xor(lastlp, 32);
+    if (mine != 0x7fffffff) { tok = mine; lpv = mlp; }
+    else if (other != 0x7fffffff) { tok = other; lpv = olp; }
+    else { tok = p.V1 - 1; lpv = ((p.V1 - 1) & 4) >> 2 == hh ? lastlp : olast; }
+    return cum;
 }
 
 template <int G, bool PAIRS, class Tail = NoTail>
@@ -1210,10 +1209,10 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         // the cell's first gate tile does not depend on the token: its loads are issued at the last logit
         // stage's mid-point (tail) and land while the token is picked
         auto tail = [&]() __attribute__((always_inline)) {
-            if (CROSS_PREFETCH && t < p.T) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
+            if (CROSS_PREFETCH && !SAMPLE && t < p.T) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
         };
         logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail);
-        cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && t < p.T;
+        cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && !SAMPLE && t < p.T;   // (SAMPLE: s64 stages the sweeps)
         PROF_MARK(120 + 24 * (t + 1));
 
         // ---- greedy token (nets.py:208-209) ------------------------------------------------
@@ -1231,9 +1230,9 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
             const double u = c.row_valid ? p.sample_u[ou] : 0.5;
             // thr = u * the row's sum of p, summed by a first sweep exactly as the walk sums (the pass-1 exp-sum
             // differs from it by ~1e-6: its exponents carry the rounding of m * log2e)
-            const double tot = sample_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, m, lse,
-                                            __builtin_inf(), tok, lp_tok);
-            sample_sweep(lds, p, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, u * tot, tok, lp_tok);
+            const double tot = sample_sweep(lds, p, nidx, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, __builtin_inf(), s64,
+                                            tok, lp_tok);
+            sample_sweep(lds, p, nidx, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, u * tot, s64, tok, lp_tok);
         } else {
             const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
             const int ci[4] = {st.r0i, st.r1i, __shfl_xor(st.r0i, 32), __shfl_xor(st.r1i, 32)};
