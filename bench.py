@@ -310,16 +310,17 @@ def main():
     G, nslabs, S_split = eng.decode_shape(B, P_local)
     path = eng.decode_path(B, P_local)
     if sampled:
-        # the sampled decode of the 5 B rows: the steps kernel (exact lse) + two logit sweeps per step for the
-        # draw's pick (the row's total of p, then the walk), one launch; the self-critical modes' greedy decode
-        # of the B images runs before it (in ms_per_step, not here)
+        # the sampled decode of the 5 B rows: the steps kernel (exact lse) + one logit sweep per step for the
+        # draw's pick (the row's total of p, keeping the groups near the threshold), one launch; a workgroup
+        # whose threshold misses its candidates sweeps again (sample_resweeps, not counted as work); the
+        # self-critical modes' greedy decode of the B images runs before it (in ms_per_step, not here)
         rows = B * spi
         G, nslabs, S_split, path = 4, (rows + 127) // 128, 1, 'fused (sampled pick)'
         kname, n_step = 'nicnes_decode_steps_kernel<sample>', 1
         step_ms = float(np.mean([q['step_ms'] for q in phases]))
-        flops = (decode_flops_per_member(rows) + 2 * logit_flops_per_member(rows)) * P_local
-        step_flop = (step_flops_per_member(rows) + 2 * logit_flops_per_member(rows)) * P_local
-        alg_bytes = (step_noise_bytes_per_member(rows) + 2 * 16 * logit_noise_bytes_per_member()) * P_local
+        flops = (decode_flops_per_member(rows) + logit_flops_per_member(rows)) * P_local
+        step_flop = (step_flops_per_member(rows) + logit_flops_per_member(rows)) * P_local
+        alg_bytes = (step_noise_bytes_per_member(rows) + 16 * logit_noise_bytes_per_member()) * P_local
     elif not ph['step_launches'] and not ph['logit_launches']:
         # two-stream decode (NICNES_DECODE_STREAMS=2): the halves' launches overlap, so the whole decode
         # is the measured unit
@@ -405,6 +406,7 @@ def main():
         'cpu_baseline': cpu,
         'decodes_per_s': round(2 * value, 3),        # one decode = one sign's rollout of the batch
         'tie_fallbacks': eng.stats()['tie_fallbacks'],
+        'sample_resweeps': eng.stats()['sample_resweeps'] if sampled else None,
         'mutation': ({'mode': args.mutation, 'vector_ms_per_iteration': round(mut_ms, 3),
                       'vector_share_of_iteration': round(mut_ms / (dt / args.steps * 1e3), 4),
                       'note': 'the per-task mutation vector, timed with events on the engine stream: SM-G-SUM '

@@ -236,7 +236,9 @@ int nicnes_allgather_fitness(nicnes_handle* h, const double* fit_local, int32_t 
  * whole population's noise sum before nicnes_adam_step (batched_weighted_sum, nic_nes_master.py:207-221). */
 int nicnes_allreduce_grad(nicnes_handle* h, float* gsum, void* stream);
 
-/* diagnostics: [0] = exact-pass fallbacks of the greedy tie rule since creation (synchronising) */
+/* diagnostics since creation (synchronising): [0] = exact-pass fallbacks of the greedy tie rule,
+ * [1] = sampled-pick workgroup steps whose threshold missed the kept candidate groups (a second sweep),
+ * [2] = coop-path hand-off timeouts */
 int nicnes_stats(nicnes_handle* h, int64_t* out4_host);
 
 /* Kernel timing with HIP events recorded on the launch stream around the decode and CIDEr-D

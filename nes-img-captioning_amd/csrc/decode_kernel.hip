@@ -69,8 +69,13 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef CROSS_PREFETCH
 #define CROSS_PREFETCH 1   // steps kernel: a phase's first staging tile loaded during the previous phase's last stage
 #endif
+#ifndef SAMPLE_BAND
+// sampled pick: relative band around the estimated threshold u * stot e^-lse within which one sweep keeps the
+// candidate groups (the exact sum differs from the estimate by the fp32 exp-sum's rounding, ~1e-6 .. 1e-5)
+#define SAMPLE_BAND 1e-4
+#endif
 #ifndef H_PREFETCH
-#define H_PREFETCH 1       // steps kernel: h_{t+1} read back from lane scratch at the end of step t
+#define H_PREFETCH 1      // steps kernel: h_{t+1} read back from lane scratch at the end of step t
 #endif
 #ifndef LOGIT_MIDSTORE
 #define LOGIT_MIDSTORE 1   // logit stages: the next stage's W+- tile is stored among the MFMAs of this one
@@ -732,17 +737,56 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
     return Sx;
 }
 
+// Candidate groups of a sampled row (sample_sweep<true>): the groups this lane owns whose cumulative
+// interval (cb, cb + gs] meets the band (lo, hi] around the row's threshold, in id order, kept in the lane
+// scratch slots the split path uses for odd-parity h' (free in the fused kernels): per candidate its four
+// (x - m) - lse, its cumulative cb (two words) and its first id. At most SAMPLE_NCAND are kept (more: the
+// walk sweep decides).
+#define SAMPLE_NCAND 8
+#define CAND_SLOT(i, f) (4u * 64u * (uint32_t)(193 + 8 * (i) + (f)))
+
+// the sampled pick inside one group of four ids (base .. base + 3) from its cumulative cb: the first id whose
+// cumulative exceeds thr (the group's last id if the fp64 sums round short of it)
+__device__ __forceinline__ void sample_group_walk(const DecodeParams& p, int base, double cb, const float (&x)[4],
+                                                  double thr, int& pick, float& plp) {
+    double c2 = cb;
+    pick = base + 3;
+    plp = x[3];
+    bool hit = false;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        c2 += base + e < p.V1 ? (double)nn_expf(x[e]) : 0.0;
+        if (!hit && c2 > thr) { hit = true; pick = base + e; plp = x[e]; }
+    }
+    pick = min(pick, p.V1 - 1);
+}
+
+// the row's pick from the two lanes' own picks (0x7fffffff: none): V1 - 1 if neither lane found one
+__device__ __forceinline__ void sample_settle(const DecodeParams& p, int hh, int mine, float mlp, float lastlp,
+                                              int& tok, float& lpv) {
+    const int other = __shfl_xor(mine, 32);
+    const float olp = __shfl_xor(mlp, 32), olast = __shfl_xor(lastlp, 32);
+    if (mine != 0x7fffffff) { tok = mine; lpv = mlp; }
+    else if (other != 0x7fffffff) { tok = other; lpv = olp; }
+    else { tok = p.V1 - 1; lpv = ((p.V1 - 1) & 4) >> 2 == hh ? lastlp : olast; }
+}
+
 // One sweep of the vocabulary in 64-row stages for the sampled pick (FCModel._sample with greedy=False,
 // nets.py:210-231; RandomState.choice: the first id whose cumulative probability exceeds the draw): the
 // row's cumulative sum of p = exp((x - m) - lse) in index order, in fp64, against thr = u * sum(p). The
 // stages are the logit loop's (two MFMA chains per wave, staged through r); a lane holds, per chain c,
 // ids 64s + 32c + 8k + 4hh + e (k, e < 4): the two lanes of a row exchange their four group sums and walk
-// the eight groups of each chain in id order; the lane holding the crossing group walks its four ids. tok /
-// lpv: the pick and its log-prob (logprobs.gather, nets.py:225); V1 - 1 if the sums never reach thr.
-// Returns the row's total of p in the same order (thr = +inf: the total alone).
+// the eight groups of each chain in id order; the lane holding the crossing group walks its four ids.
+// REC = false (the walk): tok / lpv = the pick and its log-prob (logprobs.gather, nets.py:225); V1 - 1 if
+// the sums never reach thr. REC = true (thr unused): only the total, and each lane's candidate groups for
+// any threshold in (lo, hi] go to its scratch (scr at lane offset lo4; ncand = their count), with the
+// log-prob of id V1 - 1 to lastlp.
+// Returns the row's total of p in the walk's order.
+template <bool REC>
 __device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p, uint64_t nidx, int tid, int sgn,
                                                int hh, int lane, const float (&hB)[64], float m, float lse, double thr,
-                                               Stage64Regs& r, int& tok, float& lpv) {
+                                               double lo, double hi, rsrc_t scr, uint32_t lo4, int& ncand,
+                                               float& lastlp, Stage64Regs& r, int& tok, float& lpv) {
     const int nst = (p.V1 + 63) >> 6;
     stage64_load(logit_src(p, nidx, 0), tid, r);
     stage64_store(lds, logit_src(p, nidx, 0).valid, tid, r);
@@ -750,7 +794,8 @@ __device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p
     double cum = 0.0;
     bool found = false;
     int mine = 0x7fffffff;
-    float mlp = 0.f, lastlp = 0.f;
+    float mlp = 0.f;
+    if (REC) ncand = 0;
     auto walk = [&](const f32x16& acc, int vb) __attribute__((always_inline)) {
         double g[4];
 #pragma unroll
@@ -772,24 +817,32 @@ __device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p
             const int k = j >> 1;
             const bool own = (j & 1) == hh;
             const double gs = own ? g[k] : go[k];
-            if (!found && cum + gs > thr) {
-                found = true;
-                if (own) {
-                    double c2 = cum;
-                    int pick = vb + 8 * k + 3;
-                    float plp = (acc[4 * k + 3] - m) - lse;
-                    bool hit = false;
+            if (REC) {
+                // a zero group never holds the pick: the group before it would have crossed already
+                if (own && gs > 0.0 && cum <= hi && cum + gs > lo) {
+                    if (ncand < SAMPLE_NCAND) {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const float x = (acc[4 * k + e] - m) - lse;
-                        c2 += vb + 8 * k + e < p.V1 ? (double)nn_expf(x) : 0.0;
-                        if (!hit && c2 > thr) { hit = true; pick = vb + 8 * k + e; plp = x; }
+                        for (int e = 0; e < 4; ++e) st1(scr, lo4 + CAND_SLOT(ncand, e), 0u, (acc[4 * k + e] - m) - lse);
+                        const uint64_t cbits = __builtin_bit_cast(uint64_t, cum);
+                        st1(scr, lo4 + CAND_SLOT(ncand, 4), 0u, __builtin_bit_cast(float, (uint32_t)cbits));
+                        st1(scr, lo4 + CAND_SLOT(ncand, 5), 0u, __builtin_bit_cast(float, (uint32_t)(cbits >> 32)));
+                        st1(scr, lo4 + CAND_SLOT(ncand, 6), 0u, __builtin_bit_cast(float, vb + 8 * k));
                     }
-                    mine = min(pick, p.V1 - 1);
-                    mlp = plp;
+                    ++ncand;
                 }
+                cum += gs;
+            } else {
+                if (!found && cum + gs > thr) {
+                    found = true;
+                    if (own) {
+                        float x[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) x[e] = (acc[4 * k + e] - m) - lse;
+                        sample_group_walk(p, vb + 8 * k, cum, x, thr, mine, mlp);
+                    }
+                }
+                if (!found) cum += gs;
             }
-            if (!found) cum += gs;
         }
     };
     for (int s = 0; s < nst; ++s) {
@@ -802,12 +855,40 @@ __device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p
         if (s + 1 < nst) stage64_store(lds + ((s + 1) & 1) * STAGE64_FLOATS, logit_src(p, nidx, s + 1).valid, tid, r);
         __syncthreads();
     }
-    const int other = __shfl_xor(mine, 32);
-    const float olp = __shfl_xor(mlp, 32), olast = __shfl_xor(lastlp, 32);
-    if (mine != 0x7fffffff) { tok = mine; lpv = mlp; }
-    else if (other != 0x7fffffff) { tok = other; lpv = olp; }
-    else { tok = p.V1 - 1; lpv = ((p.V1 - 1) & 4) >> 2 == hh ? lastlp : olast; }
+    if (!REC) sample_settle(p, hh, mine, mlp, lastlp, tok, lpv);
     return cum;
+}
+
+// The pick from the candidates of sample_sweep<true> at thr (in (lo, hi]): the first group in id order with
+// cb + gs > thr (gs summed again from its x as the sweep summed it), walked by its lane -- the same sums, so
+// the same pick as the walk sweep at thr.
+__device__ __forceinline__ void sample_pick_cand(const DecodeParams& p, int hh, rsrc_t scr, uint32_t lo4, int ncand,
+                                                 float lastlp, double thr, int& tok, float& lpv) {
+    int fb = 0x7fffffff;
+    double fcb = 0.0;
+    float fx[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < ncand; ++i) {
+        float x[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = ld1(scr, lo4 + CAND_SLOT(i, e), 0u);
+        const uint64_t cbits = (uint64_t)__builtin_bit_cast(uint32_t, ld1(scr, lo4 + CAND_SLOT(i, 4), 0u)) |
+                               ((uint64_t)__builtin_bit_cast(uint32_t, ld1(scr, lo4 + CAND_SLOT(i, 5), 0u)) << 32);
+        const double cb = __builtin_bit_cast(double, cbits);
+        const int base = __builtin_bit_cast(int, ld1(scr, lo4 + CAND_SLOT(i, 6), 0u));
+        double gs = 0.0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gs += base + e < p.V1 ? (double)nn_expf(x[e]) : 0.0;
+        if (cb + gs > thr) {
+            fb = base; fcb = cb;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) fx[e] = x[e];
+            break;
+        }
+    }
+    int mine = 0x7fffffff;
+    float mlp = 0.f;
+    if (fb < __shfl_xor(fb, 32)) sample_group_walk(p, fb, fcb, fx, thr, mine, mlp);
+    sample_settle(p, hh, mine, mlp, lastlp, tok, lpv);
 }
 
 template <int G, bool PAIRS, class Tail = NoTail>
@@ -1228,11 +1309,25 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         if constexpr (SAMPLE) {
             const size_t ou = (((size_t)c.member * 2 + c.sgn) * p.B + c.bc) * p.T + (t - 1);
             const double u = c.row_valid ? p.sample_u[ou] : 0.5;
-            // thr = u * the row's sum of p, summed by a first sweep exactly as the walk sums (the pass-1 exp-sum
-            // differs from it by ~1e-6: its exponents carry the rounding of m * log2e)
-            const double tot = sample_sweep(lds, p, nidx, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, __builtin_inf(), s64,
-                                            tok, lp_tok);
-            sample_sweep(lds, p, nidx, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, u * tot, s64, tok, lp_tok);
+            // thr = u * the row's sum of p, summed exactly as the walk sums (the pass-1 exp-sum stot differs from
+            // it by ~1e-6: its exponents carry the rounding of m * log2e). One sweep sums it and keeps the groups
+            // that can hold the pick for any thr within SAMPLE_BAND of u * stot e^-lse; a row whose thr falls
+            // outside (or with more candidates than kept) sends the workgroup through a second, walking sweep.
+            const double test = (double)stot * exp(-(double)lse);
+            const double blo = u * test * (1.0 - SAMPLE_BAND), bhi = u * test * (1.0 + SAMPLE_BAND);
+            int ncand = 0;
+            float lastlp = 0.f;
+            const double tot = sample_sweep<true>(lds, p, nidx, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, 0.0, blo, bhi,
+                                                  c.scr_r, lo, ncand, lastlp, s64, tok, lp_tok);
+            const double thr = u * tot;
+            const bool miss = !(thr > blo && thr <= bhi) || ncand > SAMPLE_NCAND;
+            if (__syncthreads_or((miss || p.force_exact) ? 1 : 0)) {
+                sample_sweep<false>(lds, p, nidx, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, thr, blo, bhi, c.scr_r, lo,
+                                    ncand, lastlp, s64, tok, lp_tok);
+                if (c.tid == 0) atomicAdd(p.stats + 1, 1);
+            } else {
+                sample_pick_cand(p, c.hh, c.scr_r, lo, ncand, lastlp, thr, tok, lp_tok);
+            }
         } else {
             const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
             const int ci[4] = {st.r0i, st.r1i, __shfl_xor(st.r0i, 32), __shfl_xor(st.r1i, 32)};

@@ -268,3 +268,39 @@ def test_sampled_with_member_batches_and_mutation(eng):
             _rows_agree(seq[k, s], oseq, ofr != 0)
             f_ref, _ = CR.rollout_fitness(scorer, seq[k, s], gts)
             assert abs(fit[k, s] - f_ref) <= 1e-9 * max(1.0, abs(f_ref)), (k, s)
+
+
+@pytest.mark.parametrize('gain', [1.0, 4.0])
+def test_candidate_pick_equals_the_walk_sweep(eng, monkeypatch, gain):
+    """The one-sweep pick (each row's total of p, keeping the groups near its estimated threshold) against
+    the walk sweep forced on every step (NICNES_FORCE_EXACT=1: the total, then a second sweep walking to
+    u * total): tokens and log-probs bit for bit, flat (gain 1) and peaked (gain 4) logits; the one-sweep
+    engine resweeps on few workgroup steps."""
+    import nicnes
+    dims = O.Dims()
+    theta = O.make_theta(dims, 2, gain, 0.1)
+    B = 130
+    fc = np.random.Generator(np.random.PCG64(77)).standard_normal((B, dims.F)).astype(np.float32)
+    u = np.random.Generator(np.random.PCG64(78)).random((3, 2, B, dims.T))
+    monkeypatch.setenv('NICNES_FORCE_EXACT', '1')
+    ex = nicnes.Engine(max_batch=B, max_members=3, noise_len=NOISE_LEN, noise_seed=7)
+    monkeypatch.delenv('NICNES_FORCE_EXACT')
+    out = []
+    try:
+        ex.set_noise_table(eng._table_np)
+        for e in (eng, ex):
+            _load(e, theta, fc)
+            e.set_fitness_mode('sample')
+            e.set_sample_draws(u)
+            before = e.stats()['sample_resweeps']
+            _, seq, lp = e.evaluate(9, 0, 3, SIGMA, return_seq=True, return_lp=True)
+            out.append((seq.cpu().numpy(), lp.cpu().numpy(), e.stats()['sample_resweeps'] - before))
+            e.set_sample_draws(None)
+            e.set_fitness_mode('greedy')
+    finally:
+        ex.close()
+    (s1, l1, r1), (s2, l2, r2) = out
+    assert np.array_equal(s1, s2)
+    assert np.array_equal(l1.view(np.int32), l2.view(np.int32))
+    steps = 3 * 2 * dims.T                                  # workgroup steps of the forced engine (upper bound)
+    assert r2 > 0 and r1 <= 0.1 * r2, (r1, r2, steps)
