@@ -737,6 +737,17 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
     return Sx;
 }
 
+// e^x for the sampled pick's terms: the hardware exp2 of h = fl(x log2e) corrected by the product's rounding
+// error l (x log2e = h + l to ~2^-48): exp2(h) (1 + l ln2), within ~2 ulp of e^x (nn_expf: ~1 ulp, 3x the
+// instructions; the pick compares cumulative sums, whose error stays ~1e-7 relative). 0 below e^-104.
+__device__ __forceinline__ float samp_exp(float x) {
+    const float h = x * 1.44269502162933349609375f;
+    const float l = __builtin_fmaf(x, 1.925963033500011079e-8f, __builtin_fmaf(x, 1.44269502162933349609375f, -h));
+    const float e2 = __builtin_amdgcn_exp2f(h);
+    const float y = __builtin_fmaf(e2, l * 0.693147180559945309f, e2);
+    return x > -104.f ? y : 0.f;
+}
+
 // Candidate groups of a sampled row (sample_sweep<true>): the groups this lane owns whose cumulative
 // interval (cb, cb + gs] meets the band (lo, hi] around the row's threshold, in id order, kept in the lane
 // scratch slots the split path uses for odd-parity h' (free in the fused kernels): per candidate its four
@@ -755,7 +766,7 @@ __device__ __forceinline__ void sample_group_walk(const DecodeParams& p, int bas
     bool hit = false;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-        c2 += base + e < p.V1 ? (double)nn_expf(x[e]) : 0.0;
+        c2 += base + e < p.V1 ? (double)samp_exp(x[e]) : 0.0;
         if (!hit && c2 > thr) { hit = true; pick = base + e; plp = x[e]; }
     }
     pick = min(pick, p.V1 - 1);
@@ -805,7 +816,7 @@ __device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p
             for (int e = 0; e < 4; ++e) {
                 const int v = vb + 8 * k + e;
                 const float x = (acc[4 * k + e] - m) - lse;
-                g[k] += v < p.V1 ? (double)nn_expf(x) : 0.0;
+                g[k] += v < p.V1 ? (double)samp_exp(x) : 0.0;
                 if (v == p.V1 - 1) lastlp = x;
             }
         }
@@ -877,7 +888,7 @@ __device__ __forceinline__ void sample_pick_cand(const DecodeParams& p, int hh, 
         const int base = __builtin_bit_cast(int, ld1(scr, lo4 + CAND_SLOT(i, 6), 0u));
         double gs = 0.0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) gs += base + e < p.V1 ? (double)nn_expf(x[e]) : 0.0;
+        for (int e = 0; e < 4; ++e) gs += base + e < p.V1 ? (double)samp_exp(x[e]) : 0.0;
         if (cb + gs > thr) {
             fb = base; fcb = cb;
 #pragma unroll
