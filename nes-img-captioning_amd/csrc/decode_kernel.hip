@@ -737,39 +737,41 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
     return Sx;
 }
 
-// e^x for the sampled pick's terms: the hardware exp2 of h = fl(x log2e) corrected by the product's rounding
-// error l (x log2e = h + l to ~2^-48): exp2(h) (1 + l ln2), within ~2 ulp of e^x (nn_expf: ~1 ulp, 3x the
-// instructions; the pick compares cumulative sums, whose error stays ~1e-7 relative). 0 below e^-104.
-__device__ __forceinline__ float samp_exp(float x) {
-    const float h = x * 1.44269502162933349609375f;
-    const float l = __builtin_fmaf(x, 1.925963033500011079e-8f, __builtin_fmaf(x, 1.44269502162933349609375f, -h));
-    const float e2 = __builtin_amdgcn_exp2f(h);
-    const float y = __builtin_fmaf(e2, l * 0.693147180559945309f, e2);
-    return x > -104.f ? y : 0.f;
+// The sampled pick's terms: p = e^((x - m) - lse) of logit x as exp2(x log2e - cl), cl = fl(m + lse) log2e, one
+// fma and the hardware exp2 (nn_expf: ~20 instructions). Against the oracle's fp32 (x - m) - lse: the argument's
+// rounding (~3e-7 relative per term, as the oracle's own), a tilt (x - m - lse) 1.9e-8 from log2e's fp32 rounding,
+// and cl's rounding, a common factor of every term that the threshold u * sum(p) cancels. Ids past V1 hold -inf
+// logits (bias pad): p = 0.
+__device__ __forceinline__ float samp_p(float x, float cl) {
+    return __builtin_amdgcn_exp2f(__builtin_fmaf(x, LOG2E, -cl));
 }
 
 // Candidate groups of a sampled row (sample_sweep<true>): the groups this lane owns whose cumulative
 // interval (cb, cb + gs] meets the band (lo, hi] around the row's threshold, in id order, kept in the lane
 // scratch slots the split path uses for odd-parity h' (free in the fused kernels): per candidate its four
-// (x - m) - lse, its cumulative cb (two words) and its first id. At most SAMPLE_NCAND are kept (more: the
-// walk sweep decides).
+// logits, its cumulative cb (two words) and its first id. At most SAMPLE_NCAND are kept (more: the walk
+// sweep decides).
 #define SAMPLE_NCAND 8
 #define CAND_SLOT(i, f) (4u * 64u * (uint32_t)(193 + 8 * (i) + (f)))
 
-// the sampled pick inside one group of four ids (base .. base + 3) from its cumulative cb: the first id whose
-// cumulative exceeds thr (the group's last id if the fp64 sums round short of it)
-__device__ __forceinline__ void sample_group_walk(const DecodeParams& p, int base, double cb, const float (&x)[4],
-                                                  double thr, int& pick, float& plp) {
-    double c2 = cb;
-    pick = base + 3;
-    plp = x[3];
-    bool hit = false;
+// A group's sum: its four terms added in id order in fp32 (the cumulative across groups is fp64); the walk
+// inside a group compares cb + each prefix of the same sum, so the group that crosses thr holds the pick.
+__device__ __forceinline__ float samp_group(const float (&q)[4]) {
+    return ((q[0] + q[1]) + q[2]) + q[3];
+}
+
+// the sampled pick inside one group of four ids (base .. base + 3, logits x) from its cumulative cb: the
+// first id whose cumulative exceeds thr; its log-prob (x - m) - lse (logprobs.gather, nets.py:225)
+__device__ __forceinline__ void sample_group_walk(int base, double cb, const float (&x)[4], float cl, float m,
+                                                  float lse, double thr, int& pick, float& plp) {
+    float q[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        c2 += base + e < p.V1 ? (double)samp_exp(x[e]) : 0.0;
-        if (!hit && c2 > thr) { hit = true; pick = base + e; plp = x[e]; }
-    }
-    pick = min(pick, p.V1 - 1);
+    for (int e = 0; e < 4; ++e) q[e] = samp_p(x[e], cl);
+    const float c1 = q[0] + q[1], c2 = c1 + q[2], c3 = c2 + q[3];
+    const int e = cb + (double)q[0] > thr ? 0 : cb + (double)c1 > thr ? 1 : cb + (double)c2 > thr ? 2 : 3;
+    (void)c3;
+    pick = base + e;
+    plp = (x[e] - m) - lse;
 }
 
 // the row's pick from the two lanes' own picks (0x7fffffff: none): V1 - 1 if neither lane found one
@@ -784,21 +786,22 @@ __device__ __forceinline__ void sample_settle(const DecodeParams& p, int hh, int
 
 // One sweep of the vocabulary in 64-row stages for the sampled pick (FCModel._sample with greedy=False,
 // nets.py:210-231; RandomState.choice: the first id whose cumulative probability exceeds the draw): the
-// row's cumulative sum of p = exp((x - m) - lse) in index order, in fp64, against thr = u * sum(p). The
-// stages are the logit loop's (two MFMA chains per wave, staged through r); a lane holds, per chain c,
-// ids 64s + 32c + 8k + 4hh + e (k, e < 4): the two lanes of a row exchange their four group sums and walk
-// the eight groups of each chain in id order; the lane holding the crossing group walks its four ids.
-// REC = false (the walk): tok / lpv = the pick and its log-prob (logprobs.gather, nets.py:225); V1 - 1 if
-// the sums never reach thr. REC = true (thr unused): only the total, and each lane's candidate groups for
-// any threshold in (lo, hi] go to its scratch (scr at lane offset lo4; ncand = their count), with the
-// log-prob of id V1 - 1 to lastlp.
-// Returns the row's total of p in the walk's order.
+// row's cumulative sum of p (samp_p) in index order against thr = u * sum(p), fp64 across groups of four
+// ids (samp_group). The stages are the logit loop's (two MFMA chains per wave, staged through r); a lane
+// holds, per chain c, ids 64s + 32c + 8k + 4hh + e (k, e < 4): the two lanes of a row exchange their four
+// group sums and walk the eight groups of each chain in id order; the lane holding the crossing group walks
+// its four ids.
+// REC = false (the walk): tok / lpv = the pick and its log-prob; V1 - 1 if the sums never reach thr.
+// REC = true (thr unused): only the total, and each lane's candidate groups for any threshold in (lo, hi]
+// go to its scratch (scr at lane offset lo4; ncand = their count).
+// Both: the log-prob of id V1 - 1 to lastlp. Returns the row's total of p in the walk's order.
 template <bool REC>
 __device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p, uint64_t nidx, int tid, int sgn,
                                                int hh, int lane, const float (&hB)[64], float m, float lse, double thr,
                                                double lo, double hi, rsrc_t scr, uint32_t lo4, int& ncand,
                                                float& lastlp, Stage64Regs& r, int& tok, float& lpv) {
     const int nst = (p.V1 + 63) >> 6;
+    const float cl = (m + lse) * LOG2E;
     stage64_load(logit_src(p, nidx, 0), tid, r);
     stage64_store(lds, logit_src(p, nidx, 0).valid, tid, r);
     __syncthreads();
@@ -808,53 +811,50 @@ __device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p
     float mlp = 0.f;
     if (REC) ncand = 0;
     auto walk = [&](const f32x16& acc, int vb) __attribute__((always_inline)) {
-        double g[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            g[k] = 0.0;
+        for (int k = 0; k < 4; ++k) {                    // groups (k, half 0), (k, half 1) in id order
+            float q[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int v = vb + 8 * k + e;
-                const float x = (acc[4 * k + e] - m) - lse;
-                g[k] += v < p.V1 ? (double)samp_exp(x) : 0.0;
-                if (v == p.V1 - 1) lastlp = x;
+            for (int e = 0; e < 4; ++e) q[e] = samp_p(acc[4 * k + e], cl);
+            const double g = (double)samp_group(q);
+            const double go = __shfl_xor(g, 32);
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const bool own = half == hh;
+                const double gs = own ? g : go;
+                if (REC) {
+                    // a zero group never holds the pick: the group before it would have crossed already
+                    if (own && gs > 0.0 && cum <= hi && cum + gs > lo) {
+                        if (ncand < SAMPLE_NCAND) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) st1(scr, lo4 + CAND_SLOT(ncand, e), 0u, acc[4 * k + e]);
+                            const uint64_t cbits = __builtin_bit_cast(uint64_t, cum);
+                            st1(scr, lo4 + CAND_SLOT(ncand, 4), 0u, __builtin_bit_cast(float, (uint32_t)cbits));
+                            st1(scr, lo4 + CAND_SLOT(ncand, 5), 0u, __builtin_bit_cast(float, (uint32_t)(cbits >> 32)));
+                            st1(scr, lo4 + CAND_SLOT(ncand, 6), 0u, __builtin_bit_cast(float, vb + 8 * k));
+                        }
+                        ++ncand;
+                    }
+                    cum += gs;
+                } else {
+                    if (!found && cum + gs > thr) {
+                        found = true;
+                        if (own) {
+                            float x[4];
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) x[e] = acc[4 * k + e];
+                            sample_group_walk(vb + 8 * k, cum, x, cl, m, lse, thr, mine, mlp);
+                        }
+                    }
+                    if (!found) cum += gs;
+                }
             }
         }
-        double go[4];
+    };
+    auto last_lp = [&](const f32x16& acc, int vb) __attribute__((always_inline)) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) go[k] = __shfl_xor(g[k], 32);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {                    // groups in id order: (k, half) = (j >> 1, j & 1)
-            const int k = j >> 1;
-            const bool own = (j & 1) == hh;
-            const double gs = own ? g[k] : go[k];
-            if (REC) {
-                // a zero group never holds the pick: the group before it would have crossed already
-                if (own && gs > 0.0 && cum <= hi && cum + gs > lo) {
-                    if (ncand < SAMPLE_NCAND) {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) st1(scr, lo4 + CAND_SLOT(ncand, e), 0u, (acc[4 * k + e] - m) - lse);
-                        const uint64_t cbits = __builtin_bit_cast(uint64_t, cum);
-                        st1(scr, lo4 + CAND_SLOT(ncand, 4), 0u, __builtin_bit_cast(float, (uint32_t)cbits));
-                        st1(scr, lo4 + CAND_SLOT(ncand, 5), 0u, __builtin_bit_cast(float, (uint32_t)(cbits >> 32)));
-                        st1(scr, lo4 + CAND_SLOT(ncand, 6), 0u, __builtin_bit_cast(float, vb + 8 * k));
-                    }
-                    ++ncand;
-                }
-                cum += gs;
-            } else {
-                if (!found && cum + gs > thr) {
-                    found = true;
-                    if (own) {
-                        float x[4];
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) x[e] = (acc[4 * k + e] - m) - lse;
-                        sample_group_walk(p, vb + 8 * k, cum, x, thr, mine, mlp);
-                    }
-                }
-                if (!found) cum += gs;
-            }
-        }
+        for (int i = 0; i < 16; ++i)
+            if (vb + 8 * (i >> 2) + (i & 3) == p.V1 - 1) lastlp = (acc[i] - m) - lse;
     };
     for (int s = 0; s < nst; ++s) {
         if (s + 1 < nst) stage64_load(logit_src(p, nidx, s + 1), tid, r);
@@ -863,6 +863,10 @@ __device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p
         mfma_stage64(buf + sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * sgn, hB, lane, a0, a1);
         walk(a0, 64 * s + 4 * hh);
         walk(a1, 64 * s + 32 + 4 * hh);
+        if (s + 1 == nst) {                              // id V1 - 1 lies in the last stage
+            last_lp(a0, 64 * s + 4 * hh);
+            last_lp(a1, 64 * s + 32 + 4 * hh);
+        }
         if (s + 1 < nst) stage64_store(lds + ((s + 1) & 1) * STAGE64_FLOATS, logit_src(p, nidx, s + 1).valid, tid, r);
         __syncthreads();
     }
@@ -871,25 +875,26 @@ __device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p
 }
 
 // The pick from the candidates of sample_sweep<true> at thr (in (lo, hi]): the first group in id order with
-// cb + gs > thr (gs summed again from its x as the sweep summed it), walked by its lane -- the same sums, so
-// the same pick as the walk sweep at thr.
+// cb + gs > thr (gs summed again from its logits as the sweep summed it), walked by its lane -- the same sums,
+// so the same pick as the walk sweep at thr.
 __device__ __forceinline__ void sample_pick_cand(const DecodeParams& p, int hh, rsrc_t scr, uint32_t lo4, int ncand,
-                                                 float lastlp, double thr, int& tok, float& lpv) {
+                                                 float m, float lse, float lastlp, double thr, int& tok, float& lpv) {
+    const float cl = (m + lse) * LOG2E;
     int fb = 0x7fffffff;
     double fcb = 0.0;
     float fx[4] = {0.f, 0.f, 0.f, 0.f};
     for (int i = 0; i < ncand; ++i) {
-        float x[4];
+        float x[4], q[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x[e] = ld1(scr, lo4 + CAND_SLOT(i, e), 0u);
+        for (int e = 0; e < 4; ++e) {
+            x[e] = ld1(scr, lo4 + CAND_SLOT(i, e), 0u);
+            q[e] = samp_p(x[e], cl);
+        }
         const uint64_t cbits = (uint64_t)__builtin_bit_cast(uint32_t, ld1(scr, lo4 + CAND_SLOT(i, 4), 0u)) |
                                ((uint64_t)__builtin_bit_cast(uint32_t, ld1(scr, lo4 + CAND_SLOT(i, 5), 0u)) << 32);
         const double cb = __builtin_bit_cast(double, cbits);
         const int base = __builtin_bit_cast(int, ld1(scr, lo4 + CAND_SLOT(i, 6), 0u));
-        double gs = 0.0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) gs += base + e < p.V1 ? (double)samp_exp(x[e]) : 0.0;
-        if (cb + gs > thr) {
+        if (cb + (double)samp_group(q) > thr) {
             fb = base; fcb = cb;
 #pragma unroll
             for (int e = 0; e < 4; ++e) fx[e] = x[e];
@@ -898,7 +903,7 @@ __device__ __forceinline__ void sample_pick_cand(const DecodeParams& p, int hh, 
     }
     int mine = 0x7fffffff;
     float mlp = 0.f;
-    if (fb < __shfl_xor(fb, 32)) sample_group_walk(p, fb, fcb, fx, thr, mine, mlp);
+    if (fb < __shfl_xor(fb, 32)) sample_group_walk(fb, fcb, fx, cl, m, lse, thr, mine, mlp);
     sample_settle(p, hh, mine, mlp, lastlp, tok, lpv);
 }
 
@@ -1337,7 +1342,7 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
                                     ncand, lastlp, s64, tok, lp_tok);
                 if (c.tid == 0) atomicAdd(p.stats + 1, 1);
             } else {
-                sample_pick_cand(p, c.hh, c.scr_r, lo, ncand, lastlp, thr, tok, lp_tok);
+                sample_pick_cand(p, c.hh, c.scr_r, lo, ncand, m, lse, lastlp, thr, tok, lp_tok);
             }
         } else {
             const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
