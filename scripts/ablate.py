@@ -132,7 +132,9 @@ def main():
     pop = int(os.environ.get('POP', '512'))
     B = int(os.environ.get('BATCH', '128'))
     rounds = int(os.environ.get('ROUNDS', '3'))
-    libs = sorted(glob.glob(os.path.join(REPO, 'nes-img-captioning_amd', 'build', 'ablate', 'libnicnes_*.so')))
+    # ABLATE_DIR: where the variant libraries are (build/ is not shipped to the GPU box: copy them out)
+    adir = os.environ.get('ABLATE_DIR', os.path.join(REPO, 'nes-img-captioning_amd', 'build', 'ablate'))
+    libs = sorted(glob.glob(os.path.join(adir, 'libnicnes_*.so')))
     noise = torch.from_numpy(S.noise_table(1 << 27)).cuda()
     engines = {}
     only = [x for x in os.environ.get('ONLY', '').split(',') if x]
