@@ -310,17 +310,19 @@ def main():
     G, nslabs, S_split = eng.decode_shape(B, P_local)
     path = eng.decode_path(B, P_local)
     if sampled:
-        # the sampled decode of the 5 B rows: the steps kernel (exact lse) + one logit sweep per step for the
-        # draw's pick (the row's total of p, keeping the groups near the threshold), one launch; a workgroup
-        # whose threshold misses its candidates sweeps again (sample_resweeps, not counted as work); the
-        # self-critical modes' greedy decode of the B images runs before it (in ms_per_step, not here)
+        # the sampled decode of the 5 B rows: the steps kernel (exact lse), whose logit loop also stores each
+        # step's logits in its workgroup's slot, + one pass per step reading them back for the draw's pick (the
+        # row's total of p, keeping the groups near the threshold; a wave whose threshold misses its candidates
+        # reads them again: sample_resweeps), one launch; the self-critical modes' greedy decode of the B images
+        # runs before it (in ms_per_step, not here). Bytes: the noise rows + the stored logits written and read.
         rows = B * spi
         G, nslabs, S_split, path = 4, (rows + 127) // 128, 1, 'fused (sampled pick)'
         kname, n_step = 'nicnes_decode_steps_kernel<sample>', 1
         step_ms = float(np.mean([q['step_ms'] for q in phases]))
-        flops = (decode_flops_per_member(rows) + logit_flops_per_member(rows)) * P_local
-        step_flop = (step_flops_per_member(rows) + logit_flops_per_member(rows)) * P_local
-        alg_bytes = (step_noise_bytes_per_member(rows) + 16 * logit_noise_bytes_per_member()) * P_local
+        flops = decode_flops_per_member(rows) * P_local
+        step_flop = step_flops_per_member(rows) * P_local
+        slog_bytes = 2 * 16 * 2 * (nslabs * 128) * ((9488 + 63) // 64 * 64) * 4
+        alg_bytes = (step_noise_bytes_per_member(rows) + slog_bytes) * P_local
     elif not ph['step_launches'] and not ph['logit_launches']:
         # two-stream decode (NICNES_DECODE_STREAMS=2): the halves' launches overlap, so the whole decode
         # is the measured unit

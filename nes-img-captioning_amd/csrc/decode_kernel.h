@@ -17,7 +17,12 @@ struct DecodeParams {
     const double* sample_u;      // nullable: sampled decode (nets.py:210-231, fused path only): the uniform of
                                  // every (member, sign, row, logit step) [members, 2, B, T]; NULL = greedy
     float* scratch;              // nicnes_decode_scratch_floats(): lane-private c | h' | x0 | unfinished | h' (odd)
-    int32_t* stats;              // [0] = exact-pass fallbacks (atomic), [2] = coop hand-off timeouts
+    int32_t* stats;              // [0] exact-pass fallbacks (atomic), [1] sampled re-walks, [2] coop timeouts,
+                                 // [3] sampled workgroups that found no free logit slot
+    float* slog;                 // sampled steps kernel: slog_ns logit slots of nst * 16384 floats (> one per resident
+                                 // workgroup): the logit loop stores each step's logits there, the pick reads them
+    int32_t* slog_slots;         // slog_ns claim flags (0 free), zero between launches
+    int32_t slog_ns;
     int32_t* alive;              // fused path: [members * slabs], 0 once every row of the workgroup finished
     int32_t* alive2;             // split path: [2][alive_stride] by step parity
     float* part;                 // split path: [members * slabs * S] x PART_FLOATS partial greedy states

@@ -33,6 +33,7 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 #define NTHREADS 512
@@ -746,12 +747,14 @@ __device__ __forceinline__ float samp_p(float x, float cl) {
     return __builtin_amdgcn_exp2f(__builtin_fmaf(x, LOG2E, -cl));
 }
 
-// Candidate groups of a sampled row (sample_sweep<true>): the groups this lane owns whose cumulative
+// Candidate groups of a sampled row (sample_walk_hbm<true>): the groups this lane owns whose cumulative
 // interval (cb, cb + gs] meets the band (lo, hi] around the row's threshold, in id order, kept in the lane
 // scratch slots the split path uses for odd-parity h' (free in the fused kernels): per candidate its four
 // logits, its cumulative cb (two words) and its first id. At most SAMPLE_NCAND are kept (more: the walk
 // sweep decides).
 #define SAMPLE_NCAND 8
+#define SLOG_STAGE_BYTES 65536u   // bytes of one 64-row logit stage of a workgroup in its logit slot
+#define SLOT_SPIN_TICKS 50000000ull   // 0.5 s of s_memrealtime (100 MHz) to find a free logit slot
 #define CAND_SLOT(i, f) (4u * 64u * (uint32_t)(193 + 8 * (i) + (f)))
 
 // A group's sum: its four terms added in id order in fp32 (the cumulative across groups is fp64); the walk
@@ -784,99 +787,118 @@ __device__ __forceinline__ void sample_settle(const DecodeParams& p, int hh, int
     else { tok = p.V1 - 1; lpv = ((p.V1 - 1) & 4) >> 2 == hh ? lastlp : olast; }
 }
 
-// One sweep of the vocabulary in 64-row stages for the sampled pick (FCModel._sample with greedy=False,
-// nets.py:210-231; RandomState.choice: the first id whose cumulative probability exceeds the draw): the
-// row's cumulative sum of p (samp_p) in index order against thr = u * sum(p), fp64 across groups of four
-// ids (samp_group). The stages are the logit loop's (two MFMA chains per wave, staged through r); a lane
-// holds, per chain c, ids 64s + 32c + 8k + 4hh + e (k, e < 4): the two lanes of a row exchange their four
-// group sums and walk the eight groups of each chain in id order; the lane holding the crossing group walks
-// its four ids.
+// One chain of a stage (ids from vb, lane layout as in sample_walk_hbm): REC adds its groups to cum and keeps
+// this lane's candidate groups; the walk (REC = false) stops at the first group whose cumulative crosses thr and
+// has its lane walk the group's ids (mine / mlp)
+template <bool REC>
+__device__ __forceinline__ void sample_chain(const f32x16& acc, int vb, int hh, float cl, float m, float lse,
+                                             double thr, double lo, double hi, rsrc_t scr, uint32_t lo4,
+                                             double& cum, bool& found, int& mine, float& mlp, int& ncand) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {                        // groups (k, half 0), (k, half 1) in id order
+        float q[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) q[e] = samp_p(acc[4 * k + e], cl);
+        const double g = (double)samp_group(q);
+        const double go = __shfl_xor(g, 32);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const bool own = half == hh;
+            const double gs = own ? g : go;
+            if (REC) {
+                // a zero group never holds the pick: the group before it would have crossed already
+                if (own && gs > 0.0 && cum <= hi && cum + gs > lo) {
+                    if (ncand < SAMPLE_NCAND) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) st1(scr, lo4 + CAND_SLOT(ncand, e), 0u, acc[4 * k + e]);
+                        const uint64_t cbits = __builtin_bit_cast(uint64_t, cum);
+                        st1(scr, lo4 + CAND_SLOT(ncand, 4), 0u, __builtin_bit_cast(float, (uint32_t)cbits));
+                        st1(scr, lo4 + CAND_SLOT(ncand, 5), 0u, __builtin_bit_cast(float, (uint32_t)(cbits >> 32)));
+                        st1(scr, lo4 + CAND_SLOT(ncand, 6), 0u, __builtin_bit_cast(float, vb + 8 * k));
+                    }
+                    ++ncand;
+                }
+                cum += gs;
+            } else {
+                if (!found && cum + gs > thr) {
+                    found = true;
+                    if (own) {
+                        float x[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) x[e] = acc[4 * k + e];
+                        sample_group_walk(vb + 8 * k, cum, x, cl, m, lse, thr, mine, mlp);
+                    }
+                }
+                if (!found) cum += gs;
+            }
+        }
+    }
+}
+
+// the log-prob of id V1 - 1 if this lane holds it in the chain from vb
+__device__ __forceinline__ void sample_last_lp(const DecodeParams& p, const f32x16& acc, int vb, float m, float lse,
+                                               float& lastlp) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (vb + 8 * (i >> 2) + (i & 3) == p.V1 - 1) lastlp = (acc[i] - m) - lse;
+}
+
+// The sampled pick (FCModel._sample with greedy=False, nets.py:210-231; RandomState.choice: the first id whose
+// cumulative probability exceeds the draw): one pass over the logits the logit loop stored for this step
+// (LogitStore; no GEMM, no LDS, no barrier), each lane reading back its own 32 logits per stage, one stage ahead
+// of the walk, past this CU's L1. The row's cumulative sum of p (samp_p) runs in index order against
+// thr = u * sum(p), fp64 across groups of four ids (samp_group); a lane holds, per chain c, ids
+// 64s + 32c + 8k + 4hh + e (k, e < 4): the two lanes of a row exchange their group sums and step through the
+// eight groups of each chain in id order (sample_chain).
 // REC = false (the walk): tok / lpv = the pick and its log-prob; V1 - 1 if the sums never reach thr.
 // REC = true (thr unused): only the total, and each lane's candidate groups for any threshold in (lo, hi]
 // go to its scratch (scr at lane offset lo4; ncand = their count).
 // Both: the log-prob of id V1 - 1 to lastlp. Returns the row's total of p in the walk's order.
 template <bool REC>
-__device__ __forceinline__ double sample_sweep(float* lds, const DecodeParams& p, uint64_t nidx, int tid, int sgn,
-                                               int hh, int lane, const float (&hB)[64], float m, float lse, double thr,
-                                               double lo, double hi, rsrc_t scr, uint32_t lo4, int& ncand,
-                                               float& lastlp, Stage64Regs& r, int& tok, float& lpv) {
+__device__ __forceinline__ double sample_walk_hbm(const DecodeParams& p, rsrc_t lr, uint32_t vo, int hh, float m,
+                                                  float lse, double thr, double lo, double hi, rsrc_t scr, uint32_t lo4,
+                                                  int& ncand, float& lastlp, int& tok, float& lpv) {
     const int nst = (p.V1 + 63) >> 6;
     const float cl = (m + lse) * LOG2E;
-    stage64_load(logit_src(p, nidx, 0), tid, r);
-    stage64_store(lds, logit_src(p, nidx, 0).valid, tid, r);
-    __syncthreads();
     double cum = 0.0;
     bool found = false;
     int mine = 0x7fffffff;
     float mlp = 0.f;
     if (REC) ncand = 0;
-    auto walk = [&](const f32x16& acc, int vb) __attribute__((always_inline)) {
+    auto load = [&](int s, f32x16& x0, f32x16& x1) __attribute__((always_inline)) {
+        const uint32_t so = SLOG_STAGE_BYTES * (uint32_t)s;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {                    // groups (k, half 0), (k, half 1) in id order
-            float q[4];
+        for (int k = 0; k < 4; ++k) {
+            const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(lr, (int)vo, (int)(so + 1024u * k), 16));
+            const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(lr, (int)vo, (int)(so + 1024u * (4 + k)), 16));
 #pragma unroll
-            for (int e = 0; e < 4; ++e) q[e] = samp_p(acc[4 * k + e], cl);
-            const double g = (double)samp_group(q);
-            const double go = __shfl_xor(g, 32);
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-                const bool own = half == hh;
-                const double gs = own ? g : go;
-                if (REC) {
-                    // a zero group never holds the pick: the group before it would have crossed already
-                    if (own && gs > 0.0 && cum <= hi && cum + gs > lo) {
-                        if (ncand < SAMPLE_NCAND) {
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) st1(scr, lo4 + CAND_SLOT(ncand, e), 0u, acc[4 * k + e]);
-                            const uint64_t cbits = __builtin_bit_cast(uint64_t, cum);
-                            st1(scr, lo4 + CAND_SLOT(ncand, 4), 0u, __builtin_bit_cast(float, (uint32_t)cbits));
-                            st1(scr, lo4 + CAND_SLOT(ncand, 5), 0u, __builtin_bit_cast(float, (uint32_t)(cbits >> 32)));
-                            st1(scr, lo4 + CAND_SLOT(ncand, 6), 0u, __builtin_bit_cast(float, vb + 8 * k));
-                        }
-                        ++ncand;
-                    }
-                    cum += gs;
-                } else {
-                    if (!found && cum + gs > thr) {
-                        found = true;
-                        if (own) {
-                            float x[4];
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) x[e] = acc[4 * k + e];
-                            sample_group_walk(vb + 8 * k, cum, x, cl, m, lse, thr, mine, mlp);
-                        }
-                    }
-                    if (!found) cum += gs;
-                }
-            }
+            for (int e = 0; e < 4; ++e) { x0[4 * k + e] = a[e]; x1[4 * k + e] = b[e]; }
         }
     };
-    auto last_lp = [&](const f32x16& acc, int vb) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-            if (vb + 8 * (i >> 2) + (i & 3) == p.V1 - 1) lastlp = (acc[i] - m) - lse;
-    };
-    for (int s = 0; s < nst; ++s) {
-        if (s + 1 < nst) stage64_load(logit_src(p, nidx, s + 1), tid, r);
-        const float* buf = lds + (s & 1) * STAGE64_FLOATS;
-        f32x16 a0, a1;
-        mfma_stage64(buf + sgn * (64 * LDS_ROW), buf + 2 * 64 * LDS_ROW + 64 * sgn, hB, lane, a0, a1);
-        walk(a0, 64 * s + 4 * hh);
-        walk(a1, 64 * s + 32 + 4 * hh);
-        if (s + 1 == nst) {                              // id V1 - 1 lies in the last stage
-            last_lp(a0, 64 * s + 4 * hh);
-            last_lp(a1, 64 * s + 32 + 4 * hh);
+    auto walk = [&](int s, const f32x16& x0, const f32x16& x1) __attribute__((always_inline)) {
+        sample_chain<REC>(x0, 64 * s + 4 * hh, hh, cl, m, lse, thr, lo, hi, scr, lo4, cum, found, mine, mlp, ncand);
+        sample_chain<REC>(x1, 64 * s + 32 + 4 * hh, hh, cl, m, lse, thr, lo, hi, scr, lo4, cum, found, mine, mlp, ncand);
+        if (s + 1 == nst) {
+            sample_last_lp(p, x0, 64 * s + 4 * hh, m, lse, lastlp);
+            sample_last_lp(p, x1, 64 * s + 32 + 4 * hh, m, lse, lastlp);
         }
-        if (s + 1 < nst) stage64_store(lds + ((s + 1) & 1) * STAGE64_FLOATS, logit_src(p, nidx, s + 1).valid, tid, r);
-        __syncthreads();
+    };
+    f32x16 a0, a1, b0, b1;
+    load(0, a0, a1);
+    load(min(1, nst - 1), b0, b1);
+    for (int s = 0; s < nst; s += 2) {
+        walk(s, a0, a1);
+        load(min(s + 2, nst - 1), a0, a1);               // (past the end: a repeated, unused stage)
+        if (s + 1 < nst) walk(s + 1, b0, b1);
+        load(min(s + 3, nst - 1), b0, b1);
     }
     if (!REC) sample_settle(p, hh, mine, mlp, lastlp, tok, lpv);
     return cum;
 }
 
-// The pick from the candidates of sample_sweep<true> at thr (in (lo, hi]): the first group in id order with
-// cb + gs > thr (gs summed again from its logits as the sweep summed it), walked by its lane -- the same sums,
-// so the same pick as the walk sweep at thr.
+// The pick from the candidates of sample_walk_hbm<true> at thr (in (lo, hi]): the first group in id order with
+// cb + gs > thr (gs summed again from its logits as the pass summed it), walked by its lane -- the same sums,
+// so the same pick as the walking pass at thr.
 __device__ __forceinline__ void sample_pick_cand(const DecodeParams& p, int hh, rsrc_t scr, uint32_t lo4, int ncand,
                                                  float m, float lse, float lastlp, double thr, int& tok, float& lpv) {
     const float cl = (m + lse) * LOG2E;
@@ -907,10 +929,35 @@ __device__ __forceinline__ void sample_pick_cand(const DecodeParams& p, int hh, 
     sample_settle(p, hh, mine, mlp, lastlp, tok, lpv);
 }
 
-template <int G, bool PAIRS, class Tail = NoTail>
+// logit_stages hook run after each stage's epilogue with the stage's two tiles (G = 4) and its index
+struct NoHook {
+    __device__ __forceinline__ void operator()(const f32x16&, const f32x16&, int) const {}
+};
+
+// the sampled decode's logit store: a lane's 32 logits of stage s as eight 16-byte words, word k of lane l of
+// wave w at byte s * 64 KiB + w * 8 KiB + k * 1 KiB + 16 l of the workgroup's slot (one wave instruction
+// writes 1 KiB contiguous); the walk (sample_walk_hbm) reads them back in the same lane
+struct LogitStore {
+    rsrc_t r;
+    uint32_t vo;      // 16 * lane + 8192 * wave
+    __device__ __forceinline__ void operator()(const f32x16& q0, const f32x16& q1, int s) const {
+        if (s < 0) return;                               // the pipeline's first epilogue: no stage yet
+        const uint32_t so = SLOG_STAGE_BYTES * (uint32_t)s;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const f32x4 a = {q0[4 * k], q0[4 * k + 1], q0[4 * k + 2], q0[4 * k + 3]};
+            const f32x4 b = {q1[4 * k], q1[4 * k + 1], q1[4 * k + 2], q1[4 * k + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), r, (int)vo, (int)(so + 1024u * k), 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), r, (int)vo, (int)(so + 1024u * (4 + k)), 0);
+        }
+    }
+};
+
+template <int G, bool PAIRS, class Tail = NoTail, class Hook = NoHook>
 __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, uint64_t nidx, int wave, int sgn,
                                              int hf, const float (&hB)[64], int s0, int s1, RowState& st,
-                                             Stage64Regs& s64, bool preloaded = false, Tail&& tail = Tail()) {
+                                             Stage64Regs& s64, bool preloaded = false, Tail&& tail = Tail(),
+                                             const Hook& hook = Hook()) {
     const rsrc_t lw_r = make_rsrc(p.theta + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
     const rsrc_t lz_r = make_rsrc(p.noise + nidx + p.off_log_w, 4u * 128u * (uint32_t)p.V1);
     const rsrc_t lbw_r = make_rsrc(p.theta + p.off_log_b, 4u * (uint32_t)p.V1);
@@ -964,10 +1011,12 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
                 mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
 #if !(DECODE_ABLATE & 1)
                 epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
+                hook(q0, q1, s - 1);
 #endif
             } else {
 #if !(DECODE_ABLATE & 1)
                 epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
+                hook(q0, q1, s - 1);
 #endif
                 mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
             }
@@ -990,10 +1039,12 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
 #endif
     };
     auto last = [&](const f32x16& q0, const f32x16& q1, int s) {
-        if constexpr (G == 4)
+        if constexpr (G == 4) {
             epilogue64<PAIRS>(st, q0, q1, 64 * s + vl);
-        else
+            hook(q0, q1, s);
+        } else {
             epilogue32<PAIRS>(st, q0, 64 * s + vl);
+        }
     };
     for (int s = s0; s < s1; s += 2) {
         stage(s, a0, a1, b0, b1);
@@ -1023,6 +1074,7 @@ struct Ctx {
     int tid, lane, wave, sgn, grp, hh, member, slab, b, bc, wg;
     bool row_valid;
     rsrc_t theta_r, noise_r, scr_r;
+    rsrc_t slog_r;    // sampled steps kernel: the workgroup's logit slot (else unused)
 };
 
 // a row is decoded when it lies in the slab range and in the batch's B_img * rpi rows (sign_off > 0: sign 1 takes
@@ -1265,7 +1317,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img64_kernel(DecodePar
 // s64 / pre (the steps kernel): staging registers kept across steps; pre says they hold this step's first
 // logit tile, loaded during the previous step's last cell stage (PREFETCH: that load is issued)
 // SAMPLE: the sampled decode (nets.py:210-231): the logit loop keeps only the exact (m, exp-sum), then
-// sample_sweep picks each row's token from its draw p.sample_u (fused path only)
+// sample_walk_hbm picks each row's token from its draw p.sample_u over the logits the loop stored (fused path only)
 template <bool PAIRS, bool PREFETCH, bool SAMPLE = false>
 __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, float* lds, int t, Stage64Regs& s64,
                                           bool& pre, float (&hB)[64], bool& hpre) {
@@ -1305,11 +1357,17 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         row_state_init(st);
         // the cell's first gate tile does not depend on the token: its loads are issued at the last logit
         // stage's mid-point (tail) and land while the token is picked
+        const bool xpre = CROSS_PREFETCH && t < p.T;
         auto tail = [&]() __attribute__((always_inline)) {
-            if (CROSS_PREFETCH && !SAMPLE && t < p.T) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
+            if (xpre) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
         };
-        logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail);
-        cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && !SAMPLE && t < p.T;   // (SAMPLE: s64 stages the sweeps)
+        if constexpr (SAMPLE) {                                  // the logits also go to the workgroup's slot
+            const LogitStore ls{c.slog_r, 16u * (uint32_t)lane_fresh() + 8192u * (uint32_t)c.wave};
+            logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail, ls);
+        } else {
+            logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail);
+        }
+        cell_pre = xpre && LOGIT_MIDSTORE;
         PROF_MARK(120 + 24 * (t + 1));
 
         // ---- greedy token (nets.py:208-209) ------------------------------------------------
@@ -1326,21 +1384,24 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
             const size_t ou = (((size_t)c.member * 2 + c.sgn) * p.B + c.bc) * p.T + (t - 1);
             const double u = c.row_valid ? p.sample_u[ou] : 0.5;
             // thr = u * the row's sum of p, summed exactly as the walk sums (the pass-1 exp-sum stot differs from
-            // it by ~1e-6: its exponents carry the rounding of m * log2e). One sweep sums it and keeps the groups
+            // it by ~1e-6: its exponents carry the rounding of m * log2e). One pass sums it and keeps the groups
             // that can hold the pick for any thr within SAMPLE_BAND of u * stot e^-lse; a row whose thr falls
-            // outside (or with more candidates than kept) sends the workgroup through a second, walking sweep.
+            // outside (or with more candidates than kept) sends its wave through a second, walking pass.
             const double test = (double)stot * exp(-(double)lse);
             const double blo = u * test * (1.0 - SAMPLE_BAND), bhi = u * test * (1.0 + SAMPLE_BAND);
             int ncand = 0;
             float lastlp = 0.f;
-            const double tot = sample_sweep<true>(lds, p, nidx, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, 0.0, blo, bhi,
-                                                  c.scr_r, lo, ncand, lastlp, s64, tok, lp_tok);
+            // the logit loop stored this step's logits: the passes read them back, each wave on its own (a wave
+            // whose threshold misses walks again, alone)
+            const uint32_t vo = 16u * (uint32_t)c.lane + 8192u * (uint32_t)c.wave;
+            const double tot = sample_walk_hbm<true>(p, c.slog_r, vo, c.hh, m, lse, 0.0, blo, bhi, c.scr_r, lo, ncand,
+                                                     lastlp, tok, lp_tok);
             const double thr = u * tot;
             const bool miss = !(thr > blo && thr <= bhi) || ncand > SAMPLE_NCAND;
-            if (__syncthreads_or((miss || p.force_exact) ? 1 : 0)) {
-                sample_sweep<false>(lds, p, nidx, c.tid, c.sgn, c.hh, c.lane, hB, m, lse, thr, blo, bhi, c.scr_r, lo,
-                                    ncand, lastlp, s64, tok, lp_tok);
-                if (c.tid == 0) atomicAdd(p.stats + 1, 1);
+            if (__any((miss || p.force_exact) ? 1 : 0)) {
+                sample_walk_hbm<false>(p, c.slog_r, vo, c.hh, m, lse, thr, blo, bhi, c.scr_r, lo, ncand, lastlp, tok,
+                                       lp_tok);
+                if (c.lane == 0) atomicAdd(p.stats + 1, 1);
             } else {
                 sample_pick_cand(p, c.hh, c.scr_r, lo, ncand, m, lse, lastlp, thr, tok, lp_tok);
             }
@@ -1515,16 +1576,45 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
 // workgroup setup; the state between steps stays in the same lane scratch, and a lane re-reads only
 // slots it wrote itself (a same-address store -> load of one lane: ordered like any C++ store/load pair).
 // The LDS stage buffers are free at a step boundary: every step ends on a barrier after its last read.
+// SAMPLE: the workgroup holds one of p.slog_ns logit slots for its lifetime, claimed from the slot flags at its
+// start (the first free one from its block index mod ns; fewer workgroups are resident than there are slots, one
+// per CU) and released at its end, after every wave's last read of it
 template <bool PAIRS, bool SAMPLE = false>
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodeParams p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const Ctx c = make_ctx(p);
+    Ctx c = make_ctx(p);
+    int slot = -1;
+    if constexpr (SAMPLE) {
+        __shared__ int slot_sh;
+        if (c.tid == 0) {
+            int q = (int)((blockIdx.x + blockIdx.y * gridDim.x) % (unsigned)p.slog_ns);
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (atomicCAS(p.slog_slots + q, 0, 1) != 0) {
+                q = q + 1 == p.slog_ns ? 0 : q + 1;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > SLOT_SPIN_TICKS) {   // no free slot: report, leave
+                    atomicAdd(p.stats + 3, 1);
+                    q = -1;
+                    break;
+                }
+            }
+            slot_sh = q;
+        }
+        __syncthreads();
+        slot = slot_sh;
+        if (slot < 0) return;
+        const int nst = (p.V1 + 63) >> 6;
+        c.slog_r = make_rsrc(p.slog + (size_t)slot * nst * (SLOG_STAGE_BYTES / 4), SLOG_STAGE_BYTES * (uint32_t)nst);
+    }
     wave_prio(c.wave);
     Stage64Regs s64;
     bool pre = false, hpre = false;
     float hB[64];
     for (int t = -1; t <= p.T; ++t)
         if (!step_body<PAIRS, LOGIT_MIDSTORE && CROSS_PREFETCH, SAMPLE>(p, c, lds, t, s64, pre, hB, hpre)) break;
+    if constexpr (SAMPLE) {
+        __syncthreads();                                    // every wave's reads of the slot are done
+        if (c.tid == 0) atomicExch(p.slog_slots + slot, 0);
+    }
 }
 
 // ========== split path: one member step over several workgroups =================================

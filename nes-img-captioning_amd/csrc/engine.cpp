@@ -85,6 +85,9 @@ struct nicnes_handle {
     double* su = nullptr;             // sampled modes: the draws of a decode [count, 2, B, T]
     double* base_scores = nullptr;    // self-critical modes: the greedy rows' CIDEr-D [2 count, B]
     int64_t su_cap = 0, base_cap = 0; // ... their capacities (doubles)
+    float* slog = nullptr;            // sampled modes: logit slots of the steps kernel (one per resident workgroup + spare)
+    int32_t* slog_slots = nullptr;    // ... their claim flags (zero between launches)
+    int slog_ns = 0;
     std::vector<double> su_host;      // nicnes_set_sample_draws (test hook): draws to use instead of the engine's
     int rpi = 1;                      // nicnes_set_rows_per_image: rows the sampled modes decode per image
     float* dscratch = nullptr;
@@ -405,7 +408,7 @@ int nicnes_destroy(nicnes_handle* h) {
                     h->ref_norm, h->nidx, h->seq, h->lp, h->row_scores, h->dscratch, h->stats, h->partials, h->norms,
                     h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive, h->part,
                     h->rank_key, h->rank_idx, h->mbatch, h->mut_vec, h->dbuf, h->didx, h->noise_sc, h->coop_ctr,
-                    h->zero_noise, h->zero_idx, h->sens_tok, h->su, h->base_scores};
+                    h->zero_noise, h->zero_idx, h->sens_tok, h->su, h->base_scores, h->slog, h->slog_slots};
     if (h->sens) nicnes_sens_destroy(h->sens);
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -792,6 +795,9 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
                          mode == NICNES_FITNESS_SC_LOSS;                // the criterion needs seq_logprobs
     p.lp = logprob_out ? logprob_out : (crit_lp ? h->lp : nullptr);
     p.sample_u = nullptr;
+    p.slog = nullptr;
+    p.slog_slots = nullptr;
+    p.slog_ns = 0;
     p.scratch = h->dscratch;
     p.stats = h->stats;
     p.alive = h->alive;
@@ -801,6 +807,8 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
         const int32_t fb = h->stats_host[0];
         if (h->stats_host[2] != 0)
             return fail(h, NICNES_ERR_HIP, "coop decode: a workgroup's partners never arrived (hand-off timeout)");
+        if (h->stats_host[3] != 0)
+            return fail(h, NICNES_ERR_HIP, "sampled decode: a workgroup found no free logit slot");
         if (h->last_bounded && fb - h->fb_seen >= 2) h->exact_left = 32;
         h->fb_seen = fb;
         h->stats_pending = false;
@@ -835,6 +843,21 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
                                                h->cfg.seq_length, h->su, s));
         }
         p.sample_u = h->su;
+        if (!h->slog) {
+            // a slot per resident workgroup (one per CU: the steps kernel's LDS) plus spares, each holding one
+            // step's logits of a workgroup's 2 x 128 rows (nst stages of 64 KiB)
+            const int ns = h->n_cu + 16;
+            const size_t per = (size_t)((h->V1 + 63) / 64) * 16384;
+            HIPC(h, hipDeviceSynchronize());
+            int rc = dalloc(h, &h->slog, per * ns);
+            if (!rc) rc = dalloc(h, &h->slog_slots, (size_t)ns);
+            if (rc) return rc;
+            HIPC(h, hipMemset(h->slog_slots, 0, ns * sizeof(int32_t)));
+            h->slog_ns = ns;
+        }
+        p.slog = h->slog;
+        p.slog_slots = h->slog_slots;
+        p.slog_ns = h->slog_ns;
     }
     if ((int64_t)count * nslabs * S > h->part_cap)
         return fail(h, NICNES_ERR_INVALID, "decode split beyond the partial-state buffer (nicnes_set_decode_split)");
@@ -980,6 +1003,9 @@ int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, floa
     p.coop_ctr = h->coop_ctr;
     p.coop = 0;
     p.sample_u = nullptr;
+    p.slog = nullptr;
+    p.slog_slots = nullptr;
+    p.slog_ns = 0;
     p.force_exact = h->force_exact;
     p.lse_margin = h->lse_margin;
     p.bounded_lse = 1;
