@@ -153,6 +153,11 @@ def main():
             e.set_theta(wl['theta32'])
             e.set_df_table(keys, vals, np.log(float(wl['ref_len_raw'])))
             e.set_batch(wl['fc'], wl['gts'])
+        fit = os.environ.get('FITNESS', '')    # e.g. 'sample': the sampled kernel, 5 rows per image
+        if fit:
+            e.set_fitness_mode(fit)
+            if fit in ('sample', 'self_critical', 'sc_loss'):
+                e.set_rows_per_image(5)
         e.set_timing(True)
         engines[name] = e
     res = {k: [] for k in engines}
