@@ -300,6 +300,7 @@ def test_candidate_pick_equals_the_walk_sweep(eng, monkeypatch, gain):
     finally:
         ex.close()
     (s1, l1, r1), (s2, l2, r2) = out
+    assert eng.stats()['sample_slot_timeouts'] == 0        # every workgroup found a logit slot
     assert np.array_equal(s1, s2)
     assert np.array_equal(l1.view(np.int32), l2.view(np.int32))
     steps = 3 * 2 * dims.T                                  # workgroup steps of the forced engine (upper bound)
