@@ -305,3 +305,29 @@ def test_candidate_pick_equals_the_walk_sweep(eng, monkeypatch, gain):
     assert np.array_equal(l1.view(np.int32), l2.view(np.int32))
     steps = 3 * 2 * dims.T                                  # workgroup steps of the forced engine (upper bound)
     assert r2 > 0 and r1 <= 0.1 * r2, (r1, r2, steps)
+
+
+def test_logit_slots_are_reused_across_workgroups():
+    """More sampled workgroups than logit slots (300 members x 1 slab against n_CU + 16 slots): workgroups that
+    start after others finished reuse their slots. Every member's tokens and log-probs equal the same member
+    decoded alone (a 3-member launch, no reuse), and no workgroup waited out of a slot."""
+    import nicnes
+    dims = O.Dims()
+    theta = O.make_theta(dims, 4, 4.0, 0.1)
+    B, P = 24, 300
+    e = nicnes.Engine(max_batch=B, max_members=P, noise_len=NOISE_LEN, noise_seed=7)
+    try:
+        e.set_noise_table(O.noise_table(NOISE_LEN, 123))
+        fc = np.random.Generator(np.random.PCG64(31)).standard_normal((B, dims.F)).astype(np.float32)
+        _load(e, theta, fc)
+        e.set_fitness_mode('sample')
+        _, seq, lp = e.evaluate(11, 0, P, SIGMA, return_seq=True, return_lp=True)
+        seq, lp = seq.cpu().numpy(), lp.cpu().numpy()
+        for m0 in (0, 148, 297):
+            _, s3, l3 = e.evaluate(11, m0, 3, SIGMA, return_seq=True, return_lp=True)
+            assert np.array_equal(s3.cpu().numpy(), seq[m0:m0 + 3]), m0
+            assert np.array_equal(l3.cpu().numpy().view(np.int32), lp[m0:m0 + 3].view(np.int32)), m0
+        assert e.stats()['sample_slot_timeouts'] == 0
+    finally:
+        e.set_fitness_mode('greedy')
+        e.close()
