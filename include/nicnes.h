@@ -237,7 +237,7 @@ int nicnes_allgather_fitness(nicnes_handle* h, const double* fit_local, int32_t 
 int nicnes_allreduce_grad(nicnes_handle* h, float* gsum, void* stream);
 
 /* diagnostics since creation (synchronising): [0] = exact-pass fallbacks of the greedy tie rule,
- * [1] = sampled picks whose crossing stage's own sums stopped short of the threshold by rounding (its last id),
+ * [1] = sampled-pick wave steps whose threshold missed the kept candidate groups (a second pass),
  * [2] = coop-path hand-off timeouts, [3] = sampled workgroups that found no free logit slot */
 int nicnes_stats(nicnes_handle* h, int64_t* out4_host);
 
