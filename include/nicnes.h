@@ -238,7 +238,14 @@ int nicnes_allreduce_grad(nicnes_handle* h, float* gsum, void* stream);
 
 /* diagnostics since creation (synchronising): [0] = exact-pass fallbacks of the greedy tie rule,
  * [1] = sampled-pick wave steps whose threshold missed the kept candidate groups (a second pass),
- * [2] = coop-path hand-off timeouts, [3] = sampled workgroups that found no free logit slot */
+ * [2] = coop-path hand-off timeouts, [3] = sampled workgroups that found no free logit slot.
+ * Decode faults ([2] or [3] nonzero: rows left undecoded) are sticky and contained on the device, in the
+ * iteration that hit them, without a host wait: every fitness written from then on is NaN, nicnes_grad_partial
+ * writes NaN everywhere (so an all-reduce carries the fault to every rank), and an optimizer step on this handle,
+ * or on a noise sum whose first entry is NaN, leaves theta, m and v untouched. The error (NICNES_ERR_HIP) is
+ * returned by the next evaluate that finds the counters read back, and by the ratio read of the skipped step
+ * (nicnes_adam_step / nicnes_sgd_step with ratio_out_host, nicnes_last_ratio). The handle stays faulted:
+ * destroy it (the reference's worker process dies and is restarted, main.py:107-141). */
 int nicnes_stats(nicnes_handle* h, int64_t* out4_host);
 
 /* Kernel timing with HIP events recorded on the launch stream around the decode and CIDEr-D
@@ -271,10 +278,13 @@ int nicnes_decode_shape(nicnes_handle* h, int32_t B, int32_t count, int32_t* out
  * Tokens do not depend on n. */
 int nicnes_set_decode_streams(nicnes_handle* h, int32_t n);
 /* Coop decode (not a reference interface): when the split shape has 128-row slabs, S = 2 or 4 and every
- * workgroup fits on the GPU at once (S x members x slabs <= CUs: 64 or 128 members per GPU at B = 128),
- * the whole decode runs as one persistent launch whose S workgroups per member slab hand the partial
- * greedy states and h' to each other (mode 1, the default; env NICNES_DECODE_COOP=0/1 sets the initial
- * value), instead of two launches per step (mode 0). Tokens do not depend on it. */
+ * workgroup fits on the GPU at once (S x members x slabs <= the kernel's occupancy x CUs, from
+ * hipOccupancyMaxActiveBlocksPerMultiprocessor: 64 or 128 members per GPU at B = 128), the whole decode runs
+ * as one persistent launch (env NICNES_COOP_LAUNCH=1: a cooperative launch, whose runtime check refuses a grid
+ * that cannot be resident at once; 0.4 % slower per iteration at P = 64) whose S workgroups per
+ * member slab hand the partial greedy states and h' to each other (mode 1, the default; env
+ * NICNES_DECODE_COOP=0/1 sets the initial value), instead of two launches per step (mode 0). Tokens do not
+ * depend on it. A partner missing for 0.5 s is a decode fault (nicnes_stats). */
 int nicnes_set_decode_coop(nicnes_handle* h, int32_t mode);
 
 /* SM-G-SUM sensitivity of the current theta on the first `rows` images of the batch held (batch 0):

@@ -22,7 +22,15 @@ struct CiderTables {
     uint64_t* img_hkey;        // [images, IMG_CAP] (0 = empty)
     int32_t* img_hrow;         // [images, IMG_CAP]
     double* img_vr;            // [images, IMG_ROWS, IMG_MAXR]
+    // nullable: the handle's decode counters; a coop hand-off timeout ([2]) or a sampled workgroup without a
+    // logit slot ([3]) left rows undecoded, so every fitness written from then on is NaN (decode_fault)
+    const int32_t* fault;
 };
+
+// the decode of this handle lost rows (sticky: the counters only grow; the engine reports it at the next host read)
+__device__ __forceinline__ bool decode_fault(const int32_t* f) {
+    return f != nullptr && (f[2] | f[3]) != 0;     // written by earlier launches on the stream
+}
 #define IMG_CAP 1024
 #define IMG_ROWS 512
 #define IMG_MAXR 8

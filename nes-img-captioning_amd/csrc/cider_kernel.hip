@@ -155,8 +155,13 @@ __global__ __launch_bounds__(256) void nicnes_cook_refs_kernel(const int32_t* re
 // policies.py:174-184): 100 * mean of (sample score - greedy score) per row, base = the greedy rows'
 // scores. crit 7 ('sc_loss'): LogFitnessCriterion (fitness.py:12-40), -lp * reward * mask with reward =
 // the row's self-critical score difference (policies.py:119-123, get_criterium :50-52).
+// A faulted decode (decode_fault: rows left undecoded by a hand-off or slot timeout) writes NaN instead.
 __device__ void finish_fitness(const double* row_score, const int32_t* seq, const float* lp, int B, int T, int crit,
-                               double* out, const double* base = nullptr, int base_rpi = 1) {
+                               double* out, const double* base, int base_rpi, const int32_t* fault) {
+    if (decode_fault(fault)) {
+        if (threadIdx.x == 0) *out = __builtin_nan("");
+        return;
+    }
     if (crit == 0 || crit == 5 || crit == 6 || lp == nullptr) {
         if (threadIdx.x == 0) {
             double s = 0.0;
@@ -246,7 +251,7 @@ __global__ __launch_bounds__(256) void nicnes_cider_kernel(const int32_t* seq, i
     if (scores_out)
         for (int b = threadIdx.x; b < B; b += blockDim.x) scores_out[(size_t)cand * B + b] = row_score[b];
     finish_fitness(row_score, seq + (size_t)cand * B * T, lp ? lp + (size_t)cand * B * T : nullptr, B, T, crit,
-                   fitness_out + cand, base ? base + (size_t)cand * (B / rpi) : nullptr, rpi);
+                   fitness_out + cand, base ? base + (size_t)cand * (B / rpi) : nullptr, rpi, tb.fault);
 }
 
 extern "C" uint64_t nicnes_df_hash_capacity(int64_t n) {
@@ -377,10 +382,11 @@ __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* se
 
 __global__ __launch_bounds__(256) void nicnes_cider_finish_kernel(const int32_t* seq, int B, int T,
                                                                   const double* scores, const float* lp, int crit,
-                                                                  double* fitness_out, const double* base, int rpi) {
+                                                                  double* fitness_out, const double* base, int rpi,
+                                                                  const int32_t* fault) {
     const int cand = blockIdx.x;
     finish_fitness(scores + (size_t)cand * B, seq + (size_t)cand * B * T, lp ? lp + (size_t)cand * B * T : nullptr,
-                   B, T, crit, fitness_out + cand, base ? base + (size_t)cand * (B / rpi) : nullptr, rpi);
+                   B, T, crit, fitness_out + cand, base ? base + (size_t)cand * (B / rpi) : nullptr, rpi, fault);
 }
 
 extern "C" hipError_t nicnes_launch_img_ngrams(const int32_t* img_ref_start, int B, const CiderTables* tb,
@@ -397,6 +403,6 @@ extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, in
     hipLaunchKernelGGL(nicnes_cider_img_kernel, dim3(n_cand, (B + CIDER_IMG_ROWS - 1) / CIDER_IMG_ROWS), dim3(256), 0,
                        stream, seq, B, T, *tb, img_ref_start, member_batch, scores, rpi);
     hipLaunchKernelGGL(nicnes_cider_finish_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, (const double*)scores,
-                       lp, crit, fitness_out, base, rpi);
+                       lp, crit, fitness_out, base, rpi, tb->fault);
     return hipGetLastError();
 }

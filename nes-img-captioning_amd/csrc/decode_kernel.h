@@ -28,6 +28,11 @@ struct DecodeParams {
     float* part;                 // split path: [members * slabs * S] x PART_FLOATS partial greedy states
     uint32_t* coop_ctr;          // coop path: [members * slabs] x 32 hand-off counters (zeroed per launch)
     int32_t coop;                // 1: the split shape (G = 4, S = 2 or 4) in one persistent launch
+    int32_t coop_launch;         // coop path: 1 hipLaunchCooperativeKernel (the runtime checks the grid is resident
+                                 // at once and fails the launch otherwise), 0 a plain launch of a grid the engine
+                                 // bounded by the same occupancy query (the default: same residency, no launch cost)
+    uint32_t test_stall_ms;      // test hook (NICNES_TEST_COOP_STALL): coop workgroup 0 starts this late, past the
+                                 // partners' spin bound, so they time out (0 = off)
     int32_t no_exit;             // 1: no per-slab early exit (log-probs of a multi-slab batch, see below)
     int32_t no_mask;             // 1 (fused path): feed every argmax back unmasked (forward_for_sensitivity)
     int32_t force_exact;         // test hook (NICNES_FORCE_EXACT=1): every step takes the exact tie pass
@@ -60,6 +65,10 @@ struct DecodeParams {
 // in *n_launch.
 #define DECODE_MAX_EVENTS 64
 extern "C" hipError_t nicnes_decode_init();
+// workgroups of the coop kernels (min over their instantiations) and of the sampled steps kernel one CU holds at
+// once (hipOccupancyMaxActiveBlocksPerMultiprocessor at their LDS): the coop grid must fit occ x CUs, the sampled
+// logit slots must outnumber occ x CUs
+extern "C" hipError_t nicnes_decode_occupancy(int* coop_per_cu, int* sample_per_cu);
 // shifts the per-member and per-workgroup pointers of *p to member m0 (a decode of members m0.. on
 // its own stream; nslabs = the launch's row slabs)
 extern "C" void nicnes_decode_shift(DecodeParams* p, int m0, int nslabs);

@@ -1615,6 +1615,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodePar
                     break;
                 }
             }
+            // the previous owner's stores were released before its flag store: acquire them, so this XCD's L2 holds
+            // no stale line of the slot (the slot is larger than an L2)
+            if (q >= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             slot_sh = q;
         }
         __syncthreads();
@@ -1630,8 +1633,15 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodePar
     for (int t = -1; t <= p.T; ++t)
         if (!step_body<PAIRS, LOGIT_MIDSTORE && CROSS_PREFETCH, SAMPLE>(p, c, lds, t, s64, pre, hB, hpre)) break;
     if constexpr (SAMPLE) {
-        __syncthreads();                                    // every wave's reads of the slot are done
-        if (c.tid == 0) atomicExch(p.slog_slots + slot, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's accesses of the slot are done
+        __syncthreads();
+        if (c.tid == 0) {
+            // release: this XCD's dirty lines of the slot reach HBM before another workgroup (maybe on another XCD)
+            // can claim it; the explicit vmcnt keeps the flag store behind the L2 write-back (MI355X_MICROARCH.md)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(p.slog_slots + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -2273,6 +2283,13 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_coop_kernel(DecodePara
     c.scr_r = make_rsrc(wscr, SCR_SLOTS * 64 * 4);
     uint32_t* ctr = p.coop_ctr + (size_t)gi * COOP_CTR_STRIDE;
     uint32_t phase = 0;
+    if (p.test_stall_ms && L == 0) {               // test hook: a partner that arrives past the spin bound
+        if (c.tid == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < 100000ull * p.test_stall_ms) __builtin_amdgcn_s_sleep(127);
+        }
+        __syncthreads();
+    }
     Stage64Regs s64;
     bool pre = false;
     float hB[64];
@@ -2520,6 +2537,21 @@ extern "C" hipError_t nicnes_decode_init() {
     return hipSuccess;
 }
 
+extern "C" hipError_t nicnes_decode_occupancy(int* coop_per_cu, int* sample_per_cu) {
+    const void* coop[] = {(const void*)nicnes_decode_coop_kernel<true, 2>, (const void*)nicnes_decode_coop_kernel<false, 2>,
+                          (const void*)nicnes_decode_coop_kernel<true, 4>, (const void*)nicnes_decode_coop_kernel<false, 4>};
+    int lo = 1 << 30;
+    for (const void* f : coop) {
+        int n = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, NTHREADS, LDS64);
+        if (e != hipSuccess) return e;
+        lo = n < lo ? n : lo;
+    }
+    *coop_per_cu = lo;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(sample_per_cu, (const void*)nicnes_decode_steps_kernel<false, true>,
+                                                        NTHREADS, LDS64);
+}
+
 extern "C" void nicnes_decode_shift(DecodeParams* p, int m0, int nslabs) {
     const size_t wg0 = (size_t)m0 * (size_t)nslabs;        // workgroup index wg = member * slabs + slab
     const size_t rows = (size_t)m0 * 2 * (size_t)p->B * (size_t)p->T;
@@ -2563,17 +2595,19 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
         hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(p->S, member_count, nslabs), block, LDS32, stream, *p);
         mark(DK_IMG);
         const dim3 grid(p->S * member_count * nslabs);
-        if (p->S == 2) {
-            if (pairs)
-                hipLaunchKernelGGL((nicnes_decode_coop_kernel<true, 2>), grid, block, LDS64, stream, *p, nslabs);
-            else
-                hipLaunchKernelGGL((nicnes_decode_coop_kernel<false, 2>), grid, block, LDS64, stream, *p, nslabs);
-        } else {
-            if (pairs)
-                hipLaunchKernelGGL((nicnes_decode_coop_kernel<true, 4>), grid, block, LDS64, stream, *p, nslabs);
-            else
-                hipLaunchKernelGGL((nicnes_decode_coop_kernel<false, 4>), grid, block, LDS64, stream, *p, nslabs);
-        }
+        const void* kf = p->S == 2 ? (pairs ? (const void*)nicnes_decode_coop_kernel<true, 2>
+                                            : (const void*)nicnes_decode_coop_kernel<false, 2>)
+                                   : (pairs ? (const void*)nicnes_decode_coop_kernel<true, 4>
+                                            : (const void*)nicnes_decode_coop_kernel<false, 4>);
+        DecodeParams pk = *p;
+        int ns = nslabs;
+        void* args[] = {&pk, &ns};
+        // the group hand-offs need every workgroup resident at once: the engine bounds the grid by the occupancy query
+        // (coop_fits); the cooperative launch (opt-in) has the runtime check it too and fail instead of queueing a
+        // workgroup behind its partners
+        e = p->coop_launch ? hipLaunchCooperativeKernel(kf, grid, block, args, LDS64, stream)
+                           : hipLaunchKernel(kf, grid, block, args, LDS64, stream);
+        if (e != hipSuccess) return e;
         mark(DK_COOP);
     } else if (fused) {
         if (IMG64)

@@ -114,6 +114,14 @@ struct nicnes_handle {
     // others' launch gaps and tails leave idle
     int dec_streams = 0;
     int coop_mode = 1;                // nicnes_set_decode_coop: 0 never, 1 the split shape in one launch when it fits
+    int coop_occ = 1;                 // coop kernel workgroups resident per CU (occupancy API): the grid bound
+    int sample_occ = 1;               // sampled steps kernel workgroups resident per CU: the logit slots needed
+    // NICNES_COOP_LAUNCH=1: hipLaunchCooperativeKernel for the coop kernel. The default plain launch gets the same
+    // residency from the same occupancy-bounded grid (coop_fits; MI355X_MICROARCH.md: the cooperative launch adds
+    // only the runtime's check of that bound) and costs 0.4 % less per iteration at P = 64 (r04 A/B)
+    int coop_launch = 0;
+    uint32_t test_stall_ms = 0;       // test hook NICNES_TEST_COOP_STALL (ms): coop workgroup 0 starts late
+    int test_slots = 0;               // test hook NICNES_TEST_SLOTS: this many sampled logit slots (0 = enough)
     uint32_t* coop_ctr = nullptr;     // [max_members * slabs * COOP_CTR_STRIDE] coop hand-off counters
     SensWork* sens = nullptr;         // SM-G-SUM sensitivity work buffers (nicnes_sum_sensitivity)
     float* zero_noise = nullptr;      // [D] zeros + one zero index: the sigma = 0 decode of the sensitivity
@@ -147,6 +155,7 @@ struct nicnes_handle {
     int dev_kind[DECODE_MAX_EVENTS] = {};     // kind of the launch each event follows (DK_*)
     int n_dev = 0;                            // events recorded by the last timed decode
     bool multi_stream = false;                // the last decode ran on several streams
+    bool last_nes_form = true;                // the newest optimizer step took the noise sum (not a globalg)
 };
 
 namespace {
@@ -233,7 +242,7 @@ void decode_shape(const nicnes_handle* h, int B, int count, int* G, int* nslabs,
 // The coop path (the split shape in one persistent launch, nicnes_decode_coop_kernel): 128-row slabs, 2 or
 // 4 logit ranges per member slab, and every workgroup of the launch resident at once (one per CU).
 bool coop_fits(const nicnes_handle* h, int G, int nslabs, int S, int count) {
-    return h->coop_mode && G == 4 && (S == 2 || S == 4) && (int64_t)count * nslabs * S <= h->n_cu;
+    return h->coop_mode && G == 4 && (S == 2 || S == 4) && (int64_t)count * nslabs * S <= (int64_t)h->coop_occ * h->n_cu;
 }
 
 // Buffers sized by the reference count: the cooked reference n-gram vectors (CIDEr-D).
@@ -356,6 +365,12 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
         if (ds && ds[0] >= '1' && ds[0] <= '4' && ds[1] == 0) h->dec_streams = ds[0] - '0';
         const char* dc = getenv("NICNES_DECODE_COOP");
         if (dc && (dc[0] == '0' || dc[0] == '1') && dc[1] == 0) h->coop_mode = dc[0] - '0';
+        const char* cl = getenv("NICNES_COOP_LAUNCH");
+        if (cl && (cl[0] == '0' || cl[0] == '1') && cl[1] == 0) h->coop_launch = cl[0] - '0';
+        const char* st = getenv("NICNES_TEST_COOP_STALL");
+        if (st && st[0]) h->test_stall_ms = (uint32_t)atoi(st);
+        const char* ts = getenv("NICNES_TEST_SLOTS");
+        if (ts && ts[0]) h->test_slots = atoi(ts);
     }
     {
         int ncu = 0;
@@ -363,6 +378,9 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
             h->n_cu = ncu;
     }
     if (!rc && nicnes_decode_init() != hipSuccess) rc = fail(h, NICNES_ERR_HIP, "nicnes_decode_init");
+    if (!rc && (nicnes_decode_occupancy(&h->coop_occ, &h->sample_occ) != hipSuccess || h->coop_occ < 1 ||
+                h->sample_occ < 1))
+        rc = fail(h, NICNES_ERR_HIP, "nicnes_decode_occupancy");
     if (!rc) rc = dalloc(h, &h->stats, 4);
     if (!rc && hipHostMalloc((void**)&h->stats_host, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
         rc = fail(h, NICNES_ERR_HIP, "hipHostMalloc");
@@ -511,6 +529,7 @@ static CiderTables tables_of(nicnes_handle* h) {
     tb.img_hkey = h->img_hkey;
     tb.img_hrow = h->img_hrow;
     tb.img_vr = h->img_vr;
+    tb.fault = h->stats;
     return tb;
 }
 
@@ -846,7 +865,7 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
         if (!h->slog) {
             // a slot per resident workgroup (one per CU: the steps kernel's LDS) plus spares, each holding one
             // step's logits of a workgroup's 2 x 128 rows (nst stages of 64 KiB)
-            const int ns = h->n_cu + 16;
+            const int ns = h->test_slots > 0 ? h->test_slots : h->sample_occ * h->n_cu + 16;
             const size_t per = (size_t)((h->V1 + 63) / 64) * 16384;
             HIPC(h, hipDeviceSynchronize());
             int rc = dalloc(h, &h->slog, per * ns);
@@ -865,6 +884,8 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     p.S = S;
     p.part = h->part;
     p.coop = !sampled && coop_fits(h, G, nslabs, S, count) ? 1 : 0;
+    p.coop_launch = h->coop_launch;
+    p.test_stall_ms = h->test_stall_ms;
     // log-probs of a batch spread over several slabs: every slab runs to T, then the steps after the
     // batch's last finishing step are zeroed (nicnes_lp_batch_exit), as FCModel._sample leaves them
     p.no_exit = (p.lp && nslabs > 1) ? 1 : 0;
@@ -889,9 +910,11 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     p.off_i2h_b = h->off[6];
     p.off_h2h_w = h->off[7];
     p.off_h2h_b = h->off[8];
-    // rows a member never writes (all finished early) must read as 0 (nets.py:188 zeros)
-    HIPC(h, hipMemsetAsync(p.seq, 0, (size_t)count * 2 * rows * h->cfg.seq_length * sizeof(int32_t), s));
-    if (p.lp) HIPC(h, hipMemsetAsync(p.lp, 0, (size_t)count * 2 * rows * h->cfg.seq_length * sizeof(float), s));
+    // rows a member never writes (all finished early) must read as 0 (nets.py:188 zeros). eval_theta's output is
+    // the one rollout of rows_total rows (with an odd count sign - has one row fewer than sign +)
+    const size_t out_rows = eval_theta ? (size_t)rows_total : (size_t)count * 2 * rows;
+    HIPC(h, hipMemsetAsync(p.seq, 0, out_rows * h->cfg.seq_length * sizeof(int32_t), s));
+    if (p.lp) HIPC(h, hipMemsetAsync(p.lp, 0, out_rows * h->cfg.seq_length * sizeof(float), s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[0], s));
     int n_ev = 0;
     // the coop launch needs all its workgroups resident: never split over streams
@@ -924,8 +947,7 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     h->n_dev = h->timing ? n_ev : 0;
     h->multi_stream = nstr > 1;
     if (p.no_exit)      // eval_theta: the two halves are one rollout
-        HIPC(h, nicnes_launch_lp_batch_exit(p.seq, p.lp, eval_theta ? 1 : 2 * count, eval_theta ? 2 * rows : rows_total,
-                                            h->cfg.seq_length, s));
+        HIPC(h, nicnes_launch_lp_batch_exit(p.seq, p.lp, eval_theta ? 1 : 2 * count, rows_total, h->cfg.seq_length, s));
     if (h->timing) HIPC(h, hipEventRecord(h->ev[1], s));
     if (!h->stats_pending) {          // read the fallback counter back without a host wait
         HIPC(h, hipMemcpyAsync(h->stats_host, h->stats, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -1002,6 +1024,8 @@ int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, floa
     p.part = h->part;
     p.coop_ctr = h->coop_ctr;
     p.coop = 0;
+    p.coop_launch = 1;
+    p.test_stall_ms = 0;
     p.sample_u = nullptr;
     p.slog = nullptr;
     p.slog_slots = nullptr;
@@ -1081,7 +1105,8 @@ int nicnes_grad_partial(nicnes_handle* h, uint64_t iteration, int32_t member_beg
                                       (uint64_t)h->D, h->nidx, s));
     // with a mutation the reference sums the mutated noise vectors it was sent (nic_nes_worker.py:156-161):
     // the kernel transforms each delta on the fly
-    HIPC(h, nicnes_launch_grad(h->noise, h->nidx, w, count, sigma, h->D, h->mut_vec, h->mut_mode, gsum_out, s));
+    HIPC(h, nicnes_launch_grad(h->noise, h->nidx, w, count, sigma, h->D, h->mut_vec, h->mut_mode, gsum_out, s,
+                               h->stats));
     return NICNES_OK;
 }
 
@@ -1097,8 +1122,21 @@ int nicnes_grad_partial_range(nicnes_handle* h, uint64_t iteration, int32_t memb
                                       (uint64_t)h->D, h->nidx, s));
     // the same kernel on the parameter range (slices are 64-float aligned, so j0 % 64 keeps the f32x4 loads aligned)
     HIPC(h, nicnes_launch_grad(h->noise + j0, h->nidx, w, count, sigma, j1 - j0, h->mut_vec ? h->mut_vec + j0 : nullptr,
-                               h->mut_mode, gsum_out + j0, s));
+                               h->mut_mode, gsum_out + j0, s, h->stats));
     return NICNES_OK;
+}
+
+// A skipped optimizer step (NaN ratio, nicnes_adam_kernel): say why. This handle's decode lost rows (its
+// counters), or another rank's did (the all-reduced noise sum came back NaN).
+static int fault_error(nicnes_handle* h, bool from_noise_sum = true) {
+    int32_t st[4];
+    HIPC(h, hipMemcpy(st, h->stats, sizeof st, hipMemcpyDeviceToHost));
+    if (st[2] != 0) return fail(h, NICNES_ERR_HIP, "coop decode: a workgroup's partners never arrived (hand-off timeout); "
+                                                   "the iteration's fitness is NaN and the optimizer step was skipped");
+    if (st[3] != 0) return fail(h, NICNES_ERR_HIP, "sampled decode: a workgroup found no free logit slot; "
+                                                   "the iteration's fitness is NaN and the optimizer step was skipped");
+    if (!from_noise_sum) return NICNES_OK;      // Optimizer.update(globalg) with a NaN globalg: as the reference
+    return fail(h, NICNES_ERR_HIP, "optimizer step skipped: the noise sum is NaN (a faulted decode on another rank)");
 }
 
 // one optimizer update (kind 0 Adam, 1 SGD), from the fused NES form (gsum, P, l2coeff) or from a
@@ -1135,6 +1173,8 @@ static int opt_step(nicnes_handle* h, int kind, const float* gsum, int32_t P, do
     p.one_minus_beta1_32 = (float)(1.0 - b1);
     p.one_minus_beta2_32 = (float)(1.0 - b2);
     p.epsilon = epsilon;
+    p.fault = h->stats;
+    h->last_nes_form = globalg == nullptr;
     HIPC(h, nicnes_launch_adam(&p, h->norms, s));
     h->theta_is_fp32 = 0;
     if (ratio_out_host) {
@@ -1142,6 +1182,7 @@ static int opt_step(nicnes_handle* h, int kind, const float* gsum, int32_t P, do
         HIPC(h, hipMemcpyAsync(n2, h->norms, sizeof n2, hipMemcpyDeviceToHost, s));
         HIPC(h, hipStreamSynchronize(s));
         *ratio_out_host = std::sqrt(n2[0]) / std::sqrt(n2[1]);
+        if (std::isnan(*ratio_out_host)) return fault_error(h, globalg == nullptr);
     }
     return NICNES_OK;
 }
@@ -1155,6 +1196,7 @@ int nicnes_last_ratio(nicnes_handle* h, double* ratio_out_host, void* stream) {
     HIPC(h, hipMemcpyAsync(n2, h->norms, sizeof n2, hipMemcpyDeviceToHost, s));
     HIPC(h, hipStreamSynchronize(s));
     *ratio_out_host = std::sqrt(n2[0]) / std::sqrt(n2[1]);
+    if (std::isnan(*ratio_out_host)) return fault_error(h, h->last_nes_form);
     return NICNES_OK;
 }
 

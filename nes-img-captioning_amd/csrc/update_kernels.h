@@ -22,6 +22,7 @@ struct AdamParams {
     double neg_stepsize;    // SGD: -stepsize
     const double* globalg;  // non-null: Optimizer.update(globalg) form (gsum / l2coeff unused)
     int32_t g_is_fp32;      // globalg was an fp32 array: (1 - b) * g' products stay fp32 (NEP 50)
+    const int32_t* fault;   // nullable: the handle's decode counters (decode_fault: the step is skipped)
 };
 
 extern "C" hipError_t nicnes_launch_noise_index(uint64_t seed, uint64_t iteration, uint64_t member0, int count,
@@ -37,8 +38,10 @@ extern "C" size_t nicnes_rank_scratch_pairs(int n);
 extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, uint64_t* skey, uint32_t* sidx, double* cr_out,
                                          float* w_out, hipStream_t s);
 // mode 0: delta = fp32(sigma * z); 1: delta / vec[j]; 2: delta * vec[j] (safe / proportional mutations)
+// fault (nullable): the handle's decode counters; after a faulted decode every gsum entry is NaN
 extern "C" hipError_t nicnes_launch_grad(const float* noise, const uint64_t* idx, const float* w, int count, float sigma,
-                                         int64_t dim, const float* vec, int mode, float* gsum, hipStream_t s);
+                                         int64_t dim, const float* vec, int mode, float* gsum, hipStream_t s,
+                                         const int32_t* fault = nullptr);
 extern "C" int nicnes_adam_blocks(int64_t dim);
 extern "C" hipError_t nicnes_launch_adam(const AdamParams* p, double* norms_out, hipStream_t s);
 // out[i] = fp32(sigma * in[i]), i < n (the decode's sigma-scaled noise table)

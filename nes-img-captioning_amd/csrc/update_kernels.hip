@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include "../../include/nicnes_math.h"
+#include "cider_kernel.h"
 #include "update_kernels.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -116,12 +117,19 @@ __device__ __forceinline__ float grad_delta(float sigma, float z, float v) {
     return MODE == 1 ? d / v : (MODE == 2 ? d * v : d);
 }
 
+// A faulted decode on this handle (decode_fault) poisons the sum instead: every entry NaN, so the all-reduce
+// carries the fault to every rank and each rank's optimizer step skips (nicnes_adam_kernel).
 template <int MODE>
 __global__ __launch_bounds__(256) void nicnes_grad_kernel(const float* noise, const uint64_t* idx, const float* w,
                                                           int count, float sigma, int64_t dim, const float* vec,
-                                                          float* gsum) {
+                                                          float* gsum, const int32_t* fault) {
     const int64_t j4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
     if (j4 >= dim) return;
+    if (decode_fault(fault)) {
+        for (int q = 0; q < 4; ++q)
+            if (j4 + q < dim) gsum[j4 + q] = __builtin_nanf("");
+        return;
+    }
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     const bool full = j4 + 4 <= dim;
     f32x4 v = {1.f, 1.f, 1.f, 1.f};
@@ -152,12 +160,17 @@ __global__ __launch_bounds__(256) void nicnes_grad_kernel(const float* noise, co
     if (j4 + 3 < dim) gsum[j4 + 3] = (float)a3;
 }
 
-// one Adam step; partial sums of step^2 and theta_old^2 per block for the update ratio
+// one Adam step; partial sums of step^2 and theta_old^2 per block for the update ratio.
+// No-op (theta, m, v untouched; ratio NaN) after a faulted decode: this handle's counters (p.fault), or a NaN
+// first entry of the noise sum, which a faulted rank's nicnes_grad_kernel writes and the all-reduce spreads
 __global__ __launch_bounds__(256) void nicnes_adam_kernel(AdamParams p) {
     __shared__ double red[2][256];
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double s2 = 0.0, t2 = 0.0;
-    if (j < p.dim) {
+    const bool skip = decode_fault(p.fault) || (p.gsum != nullptr && p.gsum[0] != p.gsum[0]);
+    if (skip) {
+        s2 = t2 = __builtin_nan("");
+    } else if (j < p.dim) {
         const double th = p.theta64[j];
         // globalg g' = -g + l2coeff * theta (nic_nes_master.py:311-318), or given directly
         // (Optimizer.update(globalg)). Before the first update theta, and so g', are fp32 arrays.
@@ -285,15 +298,16 @@ extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, uint64_t* ske
 }
 
 extern "C" hipError_t nicnes_launch_grad(const float* noise, const uint64_t* idx, const float* w, int count, float sigma,
-                                         int64_t dim, const float* vec, int mode, float* gsum, hipStream_t s) {
+                                         int64_t dim, const float* vec, int mode, float* gsum, hipStream_t s,
+                                         const int32_t* fault) {
     const int64_t n4 = (dim + 3) / 4;
     const dim3 grid((unsigned)((n4 + 255) / 256));
     if (mode == 1)
-        hipLaunchKernelGGL(nicnes_grad_kernel<1>, grid, dim3(256), 0, s, noise, idx, w, count, sigma, dim, vec, gsum);
+        hipLaunchKernelGGL(nicnes_grad_kernel<1>, grid, dim3(256), 0, s, noise, idx, w, count, sigma, dim, vec, gsum, fault);
     else if (mode == 2)
-        hipLaunchKernelGGL(nicnes_grad_kernel<2>, grid, dim3(256), 0, s, noise, idx, w, count, sigma, dim, vec, gsum);
+        hipLaunchKernelGGL(nicnes_grad_kernel<2>, grid, dim3(256), 0, s, noise, idx, w, count, sigma, dim, vec, gsum, fault);
     else
-        hipLaunchKernelGGL(nicnes_grad_kernel<0>, grid, dim3(256), 0, s, noise, idx, w, count, sigma, dim, vec, gsum);
+        hipLaunchKernelGGL(nicnes_grad_kernel<0>, grid, dim3(256), 0, s, noise, idx, w, count, sigma, dim, vec, gsum, fault);
     return hipGetLastError();
 }
 

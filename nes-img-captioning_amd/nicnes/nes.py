@@ -99,6 +99,12 @@ def member_batches(batch_data, member_begin, count):
 
 
 # ---------------------------------------------------------------- policy (Policy API) ------------
+class ParameterFileError(OSError):
+    """The parameter file could not be read as a state_dict: the master deletes and rewrites it between
+    iterations (nic_nes_worker.py:71-84), so a late reader can find it half written. Transient; nothing
+    else a worker raises is."""
+
+
 class EnginePolicy:
     """Policy / CaptPolicy for the engine: theta lives on the GPU (fp64 master + fp32 copy)."""
 
@@ -113,7 +119,15 @@ class EnginePolicy:
     # Policy.set_model (policies.py:125-147): PolicyNet-like object, state_dict, or .pth path
     def set_model(self, model):
         if isinstance(model, str):
-            model = torch.load(model, map_location='cpu', weights_only=True)
+            import pickle
+            try:
+                model = torch.load(model, map_location='cpu', weights_only=True)
+            except FileNotFoundError:
+                raise
+            except (EOFError, OSError, RuntimeError, pickle.UnpicklingError) as e:
+                # a truncated zip archive or pickle stream (torch.load's errors for a half-written file: a seek past
+                # the end, a missing central directory, a cut pickle)
+                raise ParameterFileError('parameter file %s unreadable: %s' % (model, e)) from e
         elif hasattr(model, 'state_dict') and not isinstance(model, dict):
             model = model.state_dict()
         if not isinstance(model, dict):

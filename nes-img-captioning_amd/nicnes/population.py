@@ -16,12 +16,14 @@ import torch.distributed as dist
 
 
 class PopulationRunner:
-    """overlap_chunks (torch.distributed exchange, world > 1): the noise sum is computed in that many
-    parameter ranges, each range's all-reduce running on the collective stream while the next range is
-    summed, so the 11.46 MB all-reduce hides behind the sum instead of following it."""
+    """Per iteration both bindings issue the same two collectives: one all-gather of the fitness and ONE
+    all-reduce of the noise sum (north_star's single all-reduce).
+    overlap_chunks > 1 (opt-in, torch.distributed exchange, world > 1; unmeasured on hardware): the noise
+    sum is computed in that many parameter ranges, each range's all-reduce running on the collective stream
+    while the next range is summed -- that many all-reduces per iteration instead of one."""
 
     def __init__(self, engine, population, sigma, l2coeff=0.0, stepsize=1e-3, beta1=0.9, beta2=0.999,
-                 epsilon=1e-08, rank=0, world_size=1, group=None, comm=None, overlap_chunks=4):
+                 epsilon=1e-08, rank=0, world_size=1, group=None, comm=None, overlap_chunks=1):
         assert population % world_size == 0, 'population must split evenly over ranks'
         self.e = engine
         self.P = population

@@ -39,7 +39,7 @@ from collections import namedtuple
 
 import numpy as np
 
-from .nes import NESTask
+from .nes import NESTask, ParameterFileError
 
 REF_MODULE = 'algorithm.nic_nes.nic_nes_master'
 
@@ -156,8 +156,10 @@ def reference_results(worker, task_id, task, member_begin, count):
 
 
 # what the reference worker survives (nic_nes_worker.py:71-84: the master deletes and rewrites the current
-# parameter file between iterations, so a late reader can find it missing or half written)
-TRANSIENT_ERRORS = (FileNotFoundError, EOFError, RuntimeError)
+# parameter file between iterations, so a late reader can find it missing or half written). Only the
+# parameter-file race: an engine error (NicnesError, e.g. a contained decode fault) or a HIP error ends the
+# worker process with a nonzero status, and the supervisor (nicnes.worker) starts a fresh one.
+TRANSIENT_ERRORS = (FileNotFoundError, ParameterFileError)
 
 
 def chunk_evals(rs, chunk, eval_prob):

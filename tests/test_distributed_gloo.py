@@ -24,20 +24,38 @@ def _free_port():
 
 
 def _run(rank, world, port, out_dir, chunks=4):
+    """chunks None: PopulationRunner's default exchange; every collective the iterations issue is counted"""
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     if world > 1:
         dist.init_process_group('gloo', rank=rank, world_size=world)
-    eng = OracleEngine(*tiny_workload())
-    r = PopulationRunner(eng, P, SIGMA, l2coeff=1e-3, stepsize=1e-2, rank=rank, world_size=world,
-                         overlap_chunks=chunks)
-    if world > 1:
-        assert len(r.ranges) == min(chunks, len(r.ranges)) and r.ranges[0][0] == 0 and r.ranges[-1][1] == eng.D
-    fits = []
-    for it in range(1, ITERS + 1):
-        f, ratio = r.step(it)
-        fits.append(f.clone().numpy())
-    np.savez(os.path.join(out_dir, 'r%d_w%d_c%d.npz' % (rank, world, chunks)), fits=np.stack(fits), theta=eng.theta32)
+    calls = {'all_reduce': 0, 'all_gather_into_tensor': 0}
+
+    def counted(name):
+        f = getattr(dist, name)
+
+        def g(*a, **k):
+            calls[name] += 1
+            return f(*a, **k)
+        return g
+    real = {n: getattr(dist, n) for n in calls}
+    for n in calls:
+        setattr(dist, n, counted(n))
+    try:
+        eng = OracleEngine(*tiny_workload())
+        kw = {} if chunks is None else {'overlap_chunks': chunks}
+        r = PopulationRunner(eng, P, SIGMA, l2coeff=1e-3, stepsize=1e-2, rank=rank, world_size=world, **kw)
+        if world > 1 and chunks is not None:
+            assert len(r.ranges) == min(chunks, len(r.ranges)) and r.ranges[0][0] == 0 and r.ranges[-1][1] == eng.D
+        fits = []
+        for it in range(1, ITERS + 1):
+            f, ratio = r.step(it)
+            fits.append(f.clone().numpy())
+    finally:
+        for n, f in real.items():
+            setattr(dist, n, f)
+    np.savez(os.path.join(out_dir, 'r%d_w%d_c%s.npz' % (rank, world, chunks)), fits=np.stack(fits), theta=eng.theta32,
+             all_reduce=calls['all_reduce'], all_gather=calls['all_gather_into_tensor'])
     if world > 1:
         dist.destroy_process_group()
 
@@ -53,6 +71,17 @@ def test_two_rank_gloo_matches_single_rank(tmp_path):
     # both ranks hold the identical replicated theta
     a, b = np.load(tmp_path / 'r0_w2_c4.npz'), np.load(tmp_path / 'r1_w2_c4.npz')
     assert np.array_equal(a['theta'], b['theta'])
+
+
+def test_default_exchange_is_one_all_gather_and_one_all_reduce(tmp_path):
+    """north_star's exchange by default: per iteration one all-gather of the fitness and ONE all-reduce of the
+    noise sum (the range overlap is opt-in), with the same result as the explicit one-chunk runner"""
+    for chunks in (None, 1):
+        mp.spawn(_run, args=(2, _free_port(), str(tmp_path), chunks), nprocs=2, join=True)
+    for rank in range(2):
+        d, one = np.load(tmp_path / ('r%d_w2_cNone.npz' % rank)), np.load(tmp_path / ('r%d_w2_c1.npz' % rank))
+        assert int(d['all_reduce']) == ITERS and int(d['all_gather']) == ITERS
+        assert np.array_equal(d['fits'], one['fits']) and np.array_equal(d['theta'], one['theta'])
 
 
 def test_overlapped_range_all_reduce_equals_one_all_reduce(tmp_path):

@@ -243,6 +243,62 @@ def test_reference_worker_survives_a_missing_parameter_file(tmp_path):
         th.join(60)
 
 
+def test_reference_worker_survives_a_half_written_parameter_file(tmp_path):
+    """A truncated .pth (the master caught mid-write) is the same transient race: ParameterFileError, logged,
+    the task re-read until the file is whole."""
+    dims, theta, fc, gts, df, n, table = tiny_workload()
+    eng = OracleEngine(dims, theta, fc, gts, df, n, table)
+    path = str(tmp_path / '0_current_params.pth')
+    torch.save(N.state_dict_from_vector(torch.from_numpy(theta), N.param_shapes(eng)), path + '.full')
+    with open(path + '.full', 'rb') as f:
+        whole = f.read()
+    with open(path, 'wb') as f:
+        f.write(whole[:len(whole) // 2])
+    with pytest.raises(N.ParameterFileError):
+        N.EnginePolicy(eng).set_model(path)
+    store = T.LocalStore()
+    mc = T.MasterClient(store, codec=W.RefPickleCodec)
+    mc.declare_experiment(_spec(4).exp)
+    batch = {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts}
+    tid = mc.declare_task(W.RefNESTask(current=path, batch_data=batch, noise_stdev=0.05, log_dir=str(tmp_path),
+                                       batch_size=4))
+    worker = N.EngineWorker(eng, _spec(4), worker_id=6)
+    stop = threading.Event()
+    th = threading.Thread(target=W.run_reference_worker, daemon=True,
+                          args=(T.WorkerClient(store, codec=W.RefPickleCodec), worker),
+                          kwargs=dict(chunk=2, seed=0, stop=stop, retry_sleep=0.01))
+    th.start()
+    try:
+        time.sleep(0.3)
+        assert th.is_alive() and mc.pop_result(timeout=0.01)[0] is None
+        os.replace(path + '.full', path)
+        t, r = mc.pop_result(timeout=60)
+        assert t == tid and r.fitness is not None
+    finally:
+        stop.set()
+        th.join(60)
+
+
+def test_reference_worker_ends_on_an_engine_error(tmp_path):
+    """An engine error is not the parameter-file race: run_reference_worker raises it (the worker process exits
+    nonzero and the supervisor starts a fresh one) instead of retrying a faulted handle forever."""
+    from nicnes._lib import NicnesError
+    dims, theta, fc, gts, df, n, table = tiny_workload()
+    eng = OracleEngine(dims, theta, fc, gts, df, n, table)
+    store = T.LocalStore()
+    mc = T.MasterClient(store, codec=W.RefPickleCodec)
+    mc.declare_experiment(_spec(4).exp)
+    batch = {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts}
+    mc.declare_task(W.RefNESTask(current=None, batch_data=batch, noise_stdev=0.05, log_dir=str(tmp_path), batch_size=4))
+    worker = N.EngineWorker(eng, _spec(4), worker_id=6)
+
+    def faulted(*a, **k):
+        raise NicnesError('coop decode: a workgroup\'s partners never arrived (hand-off timeout)')
+    worker.fitness_batch = faulted
+    with pytest.raises(NicnesError):
+        W.run_reference_worker(T.WorkerClient(store, codec=W.RefPickleCodec), worker, chunk=2, seed=0, max_tasks=1)
+
+
 def test_restart_budget_is_a_rate():
     from nicnes.worker import RestartBudget
     b = RestartBudget(2, 10.0)
