@@ -224,6 +224,33 @@ def save_df_table(path, document_frequency, ref_len_raw):
                    'ref_len': float(ref_len_raw)}, f)
 
 
+def loader_from_caption_options(exp, batch_size, seed=0, root='.'):
+    """The training loader an experiment's caption_options name (input_json, input_fc_dir, input_label_h5,
+    seq_per_img, train_only: captioning/experiment.py:9-44), at `batch_size`. Relative paths are taken from
+    `root` (the reference runs from its src/ directory). Without h5py, an .npz export next to the .h5 (same
+    stem) is read instead. Raises FileNotFoundError when the data is not there."""
+    opt = dict(exp.get('caption_options') or {})
+    for k in ('input_json', 'input_fc_dir', 'input_label_h5'):
+        if not opt.get(k):
+            raise FileNotFoundError('caption_options.%s is not set' % k)
+
+    def path(p):
+        return p if os.path.isabs(p) else os.path.join(root, p)
+    labels = path(opt['input_label_h5'])
+    npz = os.path.splitext(labels)[0] + '.npz'
+    if not labels.endswith('.npz') and os.path.exists(npz):
+        try:
+            import h5py  # noqa: F401
+        except ImportError:
+            labels = npz
+    for p in (path(opt['input_json']), path(opt['input_fc_dir']), labels):
+        if not os.path.exists(p):
+            raise FileNotFoundError(p)
+    return CocoFcDataLoader(path(opt['input_json']), path(opt['input_fc_dir']), labels, batch_size,
+                            seq_per_img=opt.get('seq_per_img') or 5, train_only=opt.get('train_only') or 0,
+                            seed=seed)
+
+
 def batches(loader, split='train', batch_size=None):
     """Endless batch stream for EngineMaster.run / run_dispatched, as the reference master draws one
     batch per iteration (nic_nes_master.py:80-96 via tools/iteration.py:150-192)."""

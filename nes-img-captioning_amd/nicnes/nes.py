@@ -220,12 +220,21 @@ class EngineWorker:
             from .mutations import batch_fc
             self.mutator.prepare((task_id, getattr(self, '_cur_version', 0)), self.e.theta()[1], batch_fc(task_data.batch_data))
 
-    def fitness_batch(self, task_id, task_data, member_begin, count):
-        """-> list of NESResult(fitness=[f+, f-] fp64, noise_idx, member)."""
+    def fitness_batch(self, task_id, task_data, member_begin, count, batches=None):
+        """-> list of NESResult(fitness=[f+, f-] fp64, noise_idx, member). batches (single_batch: false on the
+        reference wire): one batch dict per member, member k scored on batches[k] -- each drawn from the worker's
+        own loader, as each reference fitness call draws one (nic_nes_worker.py:121-128)."""
+        mb = None
+        if batches is not None:
+            if len(batches) != count:
+                raise ValueError('one batch per member: %d batches for %d members' % (len(batches), count))
+            task_data = task_data._replace(batch_data=list(batches))
+            mb = list(range(count)) if count > 1 else None
         self._prepare(task_id, task_data)
         it = int(task_data.iteration if task_data.iteration is not None else task_id)
-        fit = self.e.evaluate(it, member_begin, count, float(task_data.noise_stdev),
-                              member_batch=member_batches(task_data.batch_data, member_begin, count)).cpu().numpy()
+        if mb is None:
+            mb = member_batches(task_data.batch_data, member_begin, count)
+        fit = self.e.evaluate(it, member_begin, count, float(task_data.noise_stdev), member_batch=mb).cpu().numpy()
         idx = self.e.noise_indices(it, member_begin, count).cpu().numpy()
         return [NESResult(worker_id=self.worker_id, fitness=fit[k].copy(), noise_idx=int(idx[k]),
                           member=member_begin + k) for k in range(count)]

@@ -25,9 +25,12 @@ result.fitness / result.evolve_noise / result.eval_score (nic_nes_master.py:92-1
                iteration is (nic_nes_worker.py:65): the greedy CIDEr-D fitness of the unperturbed theta
                on the task batch stands in for the COCO validation eval, which needs java and the val
                set (out of scope).
-               Difference from reference workers with single_batch: false (mscoco_nes.json's setting):
-               they score each member on a batch of their own loader (nic_nes_worker.py:121-128); this
-               worker scores every member on the master's published batch (a warning is logged).
+               With single_batch: false (mscoco_nes.json's setting) each member is scored on a batch
+               drawn from the worker's own loader (OwnBatches), as each reference fitness call draws one
+               (nic_nes_worker.py:121-128); the SM-G-SUM sensitivity of a task is computed on the first
+               of them (the reference computes it once per task, on its first fitness call's batch:
+               nic_nes_worker.py:139-140, safe_mutations.py:34-40). Without a loader (no caption data
+               on the worker) members fall back to the published batch, with a warning.
 """
 import logging
 import io
@@ -144,10 +147,28 @@ def _rss():
         return 0
 
 
-def reference_results(worker, task_id, task, member_begin, count):
+class OwnBatches:
+    """A reference worker's own training loader (single_batch: false, nic_nes_worker.py:121-128): draw(bs)
+    returns its next training batch. When the task's batch_size differs from the loader's, the loader is
+    made anew at that size, as Experiment.increase_loader_batch_size re-runs init_loaders (a new DataLoader:
+    algorithm/tools/experiment.py:64-65, captioning/experiment.py:33-44). make_loader(batch_size) builds
+    one (e.g. nicnes.data.loader_from_caption_options)."""
+
+    def __init__(self, make_loader, batch_size):
+        self.make = make_loader
+        self.loader = make_loader(int(batch_size))
+
+    def draw(self, batch_size=None):
+        if batch_size is not None and int(batch_size) != self.loader.batch_size:
+            self.loader = self.make(int(batch_size))
+        return self.loader.get_batch('train')
+
+
+def reference_results(worker, task_id, task, member_begin, count, batches=None):
     """The engine's evaluation of members [member_begin, +count) as reference NESResults
-    (fitness = (f+, f-), evolve_noise = the member's delta)."""
-    res = worker.fitness_batch(task_id, task, member_begin, count)
+    (fitness = (f+, f-), evolve_noise = the member's delta). batches: one batch per member (own loader)."""
+    kw = {} if batches is None else {'batches': batches}
+    res = worker.fitness_batch(task_id, task, member_begin, count, **kw)
     it = int(task.iteration)
     deltas = worker.e.noise_vectors(it, member_begin, count, float(task.noise_stdev)).cpu().numpy()
     mem = _rss()
@@ -172,7 +193,7 @@ def chunk_evals(rs, chunk, eval_prob):
 
 
 def run_reference_worker(client, worker, chunk=16, eval_prob=0.0, max_tasks=None, stop=None, seed=None,
-                         idle_sleep=0.005, max_results=None, retry_sleep=0.05):
+                         idle_sleep=0.005, max_results=None, retry_sleep=0.05, own_batches=None):
     """NESWorker.run_worker (nic_nes_worker.py:41-90) against a reference master: `client` is a
     nicnes.transport.WorkerClient built with codec=RefPickleCodec. Each pass takes `chunk` slots:
     chunk_evals of them are eval results (one rollout of the unperturbed theta, pushed once per eval
@@ -180,13 +201,16 @@ def run_reference_worker(client, worker, chunk=16, eval_prob=0.0, max_tasks=None
     workers draw their noise independently; the engine needs distinct noise indices). Results of a
     task keep flowing until the master declares the next one, as reference workers do (surplus results
     are dropped by the master, nic_nes_master.py:108-116). A missing or half-written parameter file is
-    logged and the task re-read, as nic_nes_worker.py:71-84 does. Returns the number of tasks seen."""
+    logged and the task re-read, as nic_nes_worker.py:71-84 does. With single_batch: false and own_batches (an
+    OwnBatches), each member slot draws its batch from it at the task's batch_size. Returns the number of
+    tasks seen."""
     rs = random.Random(seed)
     log = logging.getLogger(__name__)
     spec = getattr(worker, 'spec', None)
-    if spec is not None and not getattr(spec, 'single_batch', True):
-        log.warning('single_batch is false: reference workers score each member on a batch of their own loader '
-                    '(nic_nes_worker.py:121-128); this worker scores every member on the published batch')
+    own = own_batches if (spec is not None and not getattr(spec, 'single_batch', True)) else None
+    if spec is not None and not getattr(spec, 'single_batch', True) and own is None:
+        log.warning('single_batch is false but this worker has no loader of its own (caption_options data): every '
+                    'member is scored on the published batch, not on one of its own (nic_nes_worker.py:121-128)')
     seen, pushed = set(), 0
     while not (stop is not None and stop.is_set()):
         task_id, ref_task = client.get_current_task()
@@ -203,8 +227,10 @@ def run_reference_worker(client, worker, chunk=16, eval_prob=0.0, max_tasks=None
                 client.push_results(task_id, [ev] * n_eval)
                 pushed += n_eval
             if chunk > n_eval:
-                begin = client.claim_members(task_id, chunk - n_eval)
-                client.push_results(task_id, reference_results(worker, task_id, task, begin, chunk - n_eval))
+                n = chunk - n_eval
+                batches = [own.draw(task.batch_size) for _ in range(n)] if own is not None else None
+                begin = client.claim_members(task_id, n)
+                client.push_results(task_id, reference_results(worker, task_id, task, begin, n, batches=batches))
                 pushed += chunk - n_eval
         except TRANSIENT_ERRORS as e:
             log.error('task %s: %s (re-reading the task)', task_id, e)

@@ -53,6 +53,8 @@ def parse_args(argv=None):
     ap.add_argument('--max_restarts', type=int, default=20, help='restarts allowed within --restart_window seconds')
     ap.add_argument('--restart_window', type=float, default=3600.0)
     ap.add_argument('--max_tasks', type=int, default=None)
+    ap.add_argument('--data_root', default='.', help="directory the experiment's caption_options paths are "
+                                                     "relative to (the reference runs from src/)")
     return ap.parse_args(argv)
 
 
@@ -114,8 +116,19 @@ def worker_main(index, device, args):
     logging.info('worker %d on device %s serving the %s wire', index, device, args.wire)
     if args.wire == 'reference':
         eval_prob = args.eval_prob if args.eval_prob is not None else float(spec.config.eval_prob or 0.0)
+        own = None
+        if not spec.single_batch:
+            # single_batch: false -- each member on a batch of this worker's own loader (nic_nes_worker.py:121-128),
+            # shuffled by its own seed as each reference worker process shuffles independently
+            from nicnes import data as Dt
+            try:
+                own = W.OwnBatches(lambda bs: Dt.loader_from_caption_options(spec.exp, bs, seed=os.getpid(),
+                                                                             root=args.data_root),
+                                   spec.batch_size)
+            except FileNotFoundError as e:
+                logging.warning('no caption data for an own loader (%s)', e)
         W.run_reference_worker(client, worker, chunk=args.chunk, eval_prob=eval_prob, stop=stop,
-                               max_tasks=args.max_tasks)
+                               max_tasks=args.max_tasks, own_batches=own)
     else:
         M.run_worker(client, worker, chunk=args.chunk, stop=stop, max_tasks=args.max_tasks)
     stop.set()

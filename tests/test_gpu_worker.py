@@ -124,3 +124,44 @@ def test_reference_wire_results_from_the_engine(tmp_path):
             assert np.array_equal(r.evolve_noise, np.float32(0.01) * table[idx: idx + e.D])
     finally:
         e.close()
+
+
+def test_reference_wire_own_batches_on_the_engine(tmp_path):
+    """single_batch: false on the reference wire, on the GPU: each member slot scores a batch of the worker's own
+    loader (builder-made caption data in the reference layout), and its result equals nicnes_evaluate_batches of
+    that member on that batch (one launch over members on different batches)"""
+    from nicnes import data as Dt, nes as N, refwire as W, transport as T
+    from tests.test_worker_entry import _caption_data
+    P, B = 6, 8
+    theta, fc, gts, df, n = _workload(B)
+    e = _engine(P, 2 * B, df, n)
+    try:
+        spec = _spec(P, B)
+        spec.exp['caption_options'] = _caption_data(tmp_path, O.Dims(), n_img=20)
+        drawn = []
+
+        def make(bs):
+            L = Dt.loader_from_caption_options(spec.exp, bs, seed=1, root=str(tmp_path))
+            get = L.get_batch
+            L.get_batch = lambda split, **kw: drawn.append(get(split, **kw)) or drawn[-1]
+            return L
+        path = str(tmp_path / '0_current_params.pth')
+        torch.save(N.state_dict_from_vector(torch.from_numpy(theta), N.param_shapes(e)), path)
+        store = T.LocalStore()
+        mc = T.MasterClient(store, codec=W.RefPickleCodec)
+        mc.declare_experiment(spec.exp)
+        tid = mc.declare_task(W.RefNESTask(current=path, batch_data={'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts},
+                                           noise_stdev=0.01, batch_size=B))
+        worker = N.EngineWorker(e, spec, worker_id=5)
+        W.run_reference_worker(T.WorkerClient(store, codec=W.RefPickleCodec), worker, chunk=3, seed=0,
+                               max_results=P, own_batches=W.OwnBatches(make, B))
+        got = np.stack([mc.pop_result(timeout=5)[1].fitness for _ in range(P)])
+        assert len(drawn) == P
+        e.set_batches([N.unique_batch(b) for b in drawn])
+        want = e.evaluate(tid, 0, P, 0.01, member_batch=list(range(P))).cpu().numpy()
+        assert np.array_equal(got, want)
+        for k in range(P):                         # and each equals the member scored alone on its batch
+            e.set_batch(*N.unique_batch(drawn[k]))
+            assert np.array_equal(e.evaluate(tid, k, 1, 0.01).cpu().numpy()[0], got[k])
+    finally:
+        e.close()

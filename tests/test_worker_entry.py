@@ -3,6 +3,7 @@ against the reference's own dist.serialize output, an engine worker serving a re
 master over it, and the `python -m nicnes.worker` pool (one process per device, spawned; a killed
 worker restarted as a fresh process) serving EngineMaster.run_dispatched across processes over a
 TCPStore. CPU only: the workers run the oracle engine (tests/worker_factory.py)."""
+import json
 import os
 import pickle
 import signal
@@ -297,6 +298,122 @@ def test_reference_worker_ends_on_an_engine_error(tmp_path):
     worker.fitness_batch = faulted
     with pytest.raises(NicnesError):
         W.run_reference_worker(T.WorkerClient(store, codec=W.RefPickleCodec), worker, chunk=2, seed=0, max_tasks=1)
+
+
+def _caption_data(tmp_path, dims, n_img=12, seed=0):
+    """A small captioning dataset in the reference's layout (cocotalk.json, fc/<id>.npy, labels): every image
+    in the train split, fc of the tiny workload's width, 5-7 label rows per image."""
+    from nicnes import data as Dt
+    rng = np.random.default_rng(seed)
+    images = [{'id': 500 + i, 'split': 'train', 'file_path': 'i%d.jpg' % i} for i in range(n_img)]
+    with open(tmp_path / 'cocotalk.json', 'w') as f:
+        json.dump({'ix_to_word': {str(i): 'w%d' % i for i in range(1, dims.vocab_size + 1)}, 'images': images}, f)
+    os.makedirs(tmp_path / 'fc', exist_ok=True)
+    for im in images:
+        np.save(tmp_path / 'fc' / ('%d.npy' % im['id']), rng.standard_normal(dims.F).astype(np.float32))
+    ncap = rng.integers(5, 8, n_img)
+    start = np.cumsum(np.concatenate([[0], ncap[:-1]])) + 1
+    labels = rng.integers(1, dims.vocab_size + 1, (int(ncap.sum()), 16))
+    labels[:, 9:] = 0
+    Dt.LabelStore(labels, start, start + ncap - 1).save_npz(str(tmp_path / 'cocotalk_label.npz'))
+    return {'input_json': 'cocotalk.json', 'input_fc_dir': 'fc', 'input_label_h5': 'cocotalk_label.h5'}
+
+
+def test_reference_worker_draws_own_batches_when_single_batch_is_false(tmp_path):
+    """single_batch: false (mscoco_nes.json) on the reference wire: every member slot scores a batch of the
+    worker's own loader, drawn at the task's batch_size (the loader re-made when it differs, as
+    increase_loader_batch_size does), and each result equals the engine's per-member-batch evaluation
+    (nicnes_evaluate_batches) of that member on that batch."""
+    from nicnes import data as Dt
+    dims, theta, fc, gts, df, n, table = tiny_workload()
+    eng = OracleEngine(dims, theta, fc, gts, df, n, table)
+    copts = _caption_data(tmp_path, dims)
+    spec = _spec(6, bs=4, single_batch=False)
+    spec.exp['caption_options'] = copts
+    drawn, sizes = [], []
+
+    def make(bs):
+        sizes.append(bs)
+        L = Dt.loader_from_caption_options(spec.exp, bs, seed=7, root=str(tmp_path))
+        get = L.get_batch
+
+        def rec(split, **kw):
+            b = get(split, **kw)
+            drawn.append(b)
+            return b
+        L.get_batch = rec
+        return L
+    own = W.OwnBatches(make, spec.batch_size)
+    path = str(tmp_path / 'p.pth')
+    torch.save(N.state_dict_from_vector(torch.from_numpy(theta), N.param_shapes(eng)), path)
+    store = T.LocalStore()
+    mc = T.MasterClient(store, codec=W.RefPickleCodec)
+    mc.declare_experiment(spec.exp)
+    pub = {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts}              # the published batch (not used)
+    tid = mc.declare_task(W.RefNESTask(current=path, batch_data=pub, noise_stdev=0.05, log_dir=str(tmp_path),
+                                       batch_size=5))
+    worker = N.EngineWorker(eng, spec, worker_id=9)
+    W.run_reference_worker(T.WorkerClient(store, codec=W.RefPickleCodec), worker, chunk=3, seed=0,
+                           max_results=6, own_batches=own)
+    assert sizes == [4, 5]                                   # made at config.batch_size, re-made at the task's
+    assert len(drawn) == 6 and all(len(b['gts']) == 5 for b in drawn)
+    ids = [tuple(i['id'] for i in b['infos']) for b in drawn]
+    assert all(ids[k] != ids[k + 1] for k in range(5))       # consecutive slots: different images
+    res = []
+    while True:
+        t, r = mc.pop_result(timeout=0.01)
+        if t is None:
+            break
+        assert t == tid
+        res.append(r)
+    assert len(res) == 6
+    ref = OracleEngine(dims, theta, fc, gts, df, n, table)
+    ref.set_batches([N.unique_batch(b) for b in drawn])
+    want = ref.evaluate(tid, 0, 6, 0.05, member_batch=list(range(6))).numpy()
+    got = np.stack([r.fitness for r in res])
+    assert np.array_equal(got, want)
+    assert not np.array_equal(got[0], got[1])
+
+
+def test_own_batches_sm_g_sum_sensitivity_from_the_first_drawn_batch(tmp_path):
+    """SM-G-SUM with single_batch: false: the task's sensitivity is computed once, on the first batch the worker
+    drew for it (the reference's first fitness call of the task computes and caches it, nic_nes_worker.py:137-140,
+    safe_mutations.py:34-40), and every member's noise is divided by it"""
+    from nicnes import data as Dt
+    dims, theta, fc, gts, df, n, table = tiny_workload()
+    eng = OracleEngine(dims, theta, fc, gts, df, n, table)
+    exp = dict(_spec(4, bs=4, single_batch=False).exp)
+    exp['policy_options'] = {'net': 'fc_caption', 'fitness': 'greedy',
+                             'model_options': {'safe_mutations': 'SM-G-SUM', 'safe_mutation_underflow': 0.1}}
+    exp['caption_options'] = _caption_data(tmp_path, dims)
+    spec = C.ExperimentSpec(exp, vocab_size=63)
+    drawn = []
+
+    def make(bs):
+        L = Dt.loader_from_caption_options(spec.exp, bs, seed=3, root=str(tmp_path))
+        get = L.get_batch
+        L.get_batch = lambda split, **kw: drawn.append(get(split, **kw)) or drawn[-1]
+        return L
+    path = str(tmp_path / 'p.pth')
+    torch.save(N.state_dict_from_vector(torch.from_numpy(theta), N.param_shapes(eng)), path)
+    store = T.LocalStore()
+    mc = T.MasterClient(store, codec=W.RefPickleCodec)
+    mc.declare_experiment(spec.exp)
+    tid = mc.declare_task(W.RefNESTask(current=path, batch_data={'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts},
+                                       noise_stdev=0.05, log_dir=str(tmp_path), batch_size=4))
+    worker = N.EngineWorker(eng, spec, worker_id=9)
+    W.run_reference_worker(T.WorkerClient(store, codec=W.RefPickleCodec), worker, chunk=2, seed=0,
+                           max_results=4, own_batches=W.OwnBatches(make, 4))
+    assert len(drawn) == 4
+    ref = OracleEngine(dims, theta, fc, gts, df, n, table)
+    ref.set_batches([N.unique_batch(drawn[0])])
+    want_s = ref.sum_sensitivity(4, 0.1)
+    assert torch.equal(worker.mutator.vector, want_s)
+    ref.set_mutation('divide', want_s)
+    ref.set_batches([N.unique_batch(b) for b in drawn])
+    want = ref.evaluate(tid, 0, 4, 0.05, member_batch=[0, 1, 2, 3]).numpy()
+    got = np.stack([mc.pop_result(timeout=0.01)[1].fitness for _ in range(4)])
+    assert np.array_equal(got, want)
 
 
 def test_restart_budget_is_a_rate():
