@@ -310,18 +310,17 @@ def main():
     G, nslabs, S_split = eng.decode_shape(B, P_local)
     path = eng.decode_path(B, P_local)
     if sampled:
-        # the sampled decode of the 5 B rows: the steps kernel (exact lse), whose logit loop also stores each
-        # step's logits in its workgroup's slot, + one pass per step reading them back for the draw's pick (the
-        # row's total of p, keeping the groups near the threshold; a wave whose threshold misses its candidates
-        # reads them again: sample_resweeps), one launch; the self-critical modes' greedy decode of the B images
-        # runs before it (in ms_per_step, not here). Bytes: the noise rows + the stored logits written and read.
+        # the sampled decode of the 5 B rows: the steps kernel, whose logit loop also stores each step's logits and
+        # per-stage sums of p in its workgroup's slot; the pick scans the stage sums and walks one stage's logits
+        # (one launch); the self-critical modes' greedy decode of the B images runs before it (in ms_per_step,
+        # not here). Bytes: the noise rows + the stored logits written (their read-back is one stage per row).
         rows = B * spi
         G, nslabs, S_split, path = 4, (rows + 127) // 128, 1, 'fused (sampled pick)'
         kname, n_step = 'nicnes_decode_steps_kernel<sample>', 1
         step_ms = float(np.mean([q['step_ms'] for q in phases]))
         flops = decode_flops_per_member(rows) * P_local
         step_flop = step_flops_per_member(rows) * P_local
-        slog_bytes = 2 * 16 * 2 * (nslabs * 128) * ((9488 + 63) // 64 * 64) * 4
+        slog_bytes = 16 * 2 * (nslabs * 128) * ((9488 + 63) // 64 * 64) * 4
         alg_bytes = (step_noise_bytes_per_member(rows) + slog_bytes) * P_local
     elif not ph['step_launches'] and not ph['logit_launches']:
         # two-stream decode (NICNES_DECODE_STREAMS=2): the halves' launches overlap, so the whole decode
@@ -408,7 +407,7 @@ def main():
         'cpu_baseline': cpu,
         'decodes_per_s': round(2 * value, 3),        # one decode = one sign's rollout of the batch
         'tie_fallbacks': eng.stats()['tie_fallbacks'],
-        'sample_resweeps': eng.stats()['sample_resweeps'] if sampled else None,
+        'sample_stage_fallbacks': eng.stats()['sample_stage_fallbacks'] if sampled else None,
         'mutation': ({'mode': args.mutation, 'vector_ms_per_iteration': round(mut_ms, 3),
                       'vector_share_of_iteration': round(mut_ms / (dt / args.steps * 1e3), 4),
                       'note': 'the per-task mutation vector, timed with events on the engine stream: SM-G-SUM '

@@ -237,7 +237,7 @@ int nicnes_allgather_fitness(nicnes_handle* h, const double* fit_local, int32_t 
 int nicnes_allreduce_grad(nicnes_handle* h, float* gsum, void* stream);
 
 /* diagnostics since creation (synchronising): [0] = exact-pass fallbacks of the greedy tie rule,
- * [1] = sampled-pick wave steps whose threshold missed the kept candidate groups (a second pass),
+ * [1] = sampled picks whose crossing stage's own sums stopped short of the threshold by rounding (its last id),
  * [2] = coop-path hand-off timeouts, [3] = sampled workgroups that found no free logit slot.
  * Decode faults ([2] or [3] nonzero: rows left undecoded) are sticky and contained on the device, in the
  * iteration that hit them, without a host wait: every fitness written from then on is NaN, nicnes_grad_partial

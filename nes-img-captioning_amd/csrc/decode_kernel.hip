@@ -70,11 +70,6 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef CROSS_PREFETCH
 #define CROSS_PREFETCH 1   // steps kernel: a phase's first staging tile loaded during the previous phase's last stage
 #endif
-#ifndef SAMPLE_BAND
-// sampled pick: relative band around the estimated threshold u * stot e^-lse within which one sweep keeps the
-// candidate groups (the exact sum differs from the estimate by the fp32 exp-sum's rounding, ~1e-6 .. 1e-5)
-#define SAMPLE_BAND 1e-4
-#endif
 #ifndef H_PREFETCH
 #define H_PREFETCH 1      // steps kernel: h_{t+1} read back from lane scratch at the end of step t
 #endif
@@ -738,226 +733,57 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
     return Sx;
 }
 
-// The sampled pick's terms: p = e^((x - m) - lse) of logit x as exp2(x log2e - cl), cl = fl(m + lse) log2e, one
-// fma and the hardware exp2 (nn_expf: ~20 instructions). Against the oracle's fp32 (x - m) - lse: the argument's
-// rounding (~3e-7 relative per term, as the oracle's own), a tilt (x - m - lse) 1.9e-8 from log2e's fp32 rounding,
-// and cl's rounding, a common factor of every term that the threshold u * sum(p) cancels. Ids past V1 hold -inf
-// logits (bias pad): p = 0.
-__device__ __forceinline__ float samp_p(float x, float cl) {
-    return __builtin_amdgcn_exp2f(__builtin_fmaf(x, LOG2E, -cl));
+// ---- sampled pick (FCModel._sample with greedy=False, nets.py:210-231) ------------------------------
+// RandomState.choice takes the first id whose cumulative probability exceeds the draw u. Here the terms are
+// p = exp2(fma(x, log2e, -r)) of logit x relative to an integer reference r >= max x * log2e (each lane's own,
+// raised as its running max grows), scaled to a common reference R by exact powers of two: 2^(r - R) p. In
+// proportion they are e^x (the normalisation cancels in u * sum(p)); against the oracle's exp((x - m) - lse)
+// each differs by the argument's rounding (~3e-7 relative, as the oracle's own) and a tilt x 1.9e-8 from
+// log2e's fp32 rounding. Four ids are summed in fp32 (a group), groups and stages in fp64.
+//
+// The logit loop writes every stage's logits to the workgroup's HBM slot (SampleStage) together with each
+// lane's stage partial sum P (its 8 groups) and its r; its running total T (fp64, exact rescales) gives
+// the row's sum(p) when the loop ends. The pick then scans the 149 stage sums (16 bytes per lane and stage)
+// for the stage where the cumulative crosses u * T, and walks that stage's 64 logits id by id.
+//
+// Slot layout per stage: [wave][word 0..8][lane] x 16 bytes; words 0-3 / 4-7 the lane's logits of chain a /
+// b (16 each), word 8 = {P (fp64), r, 0}.
+#define SLOG_WAVE_BYTES 9216u                  // 9 words x 64 lanes x 16 bytes
+#define SLOG_STAGE_BYTES (8u * SLOG_WAVE_BYTES)  // one 64-row stage of a workgroup (72 KiB)
+#define SLOT_SPIN_TICKS 50000000ull   // 0.5 s of s_memrealtime (100 MHz) to find a free logit slot
+
+__device__ __forceinline__ float samp_p(float x, float ref) {
+    return __builtin_amdgcn_exp2f(__builtin_fmaf(x, LOG2E, -ref));
 }
 
-// Candidate groups of a sampled row (sample_walk_hbm<true>): the groups this lane owns whose cumulative
-// interval (cb, cb + gs] meets the band (lo, hi] around the row's threshold, in id order, kept in the lane
-// scratch slots the split path uses for odd-parity h' (free in the fused kernels): per candidate its four
-// logits, its cumulative cb (two words) and its first id. At most SAMPLE_NCAND are kept (more: the walk
-// sweep decides).
-#define SAMPLE_NCAND 8
-#define SLOG_STAGE_BYTES 65536u   // bytes of one 64-row logit stage of a workgroup in its logit slot
-#ifndef SLOG_DEPTH
-#define SLOG_DEPTH 3      // stages of stored logits in flight per lane in the sampled pass (2 or 3; 3: -1.3 %)
-#endif
-#define SLOT_SPIN_TICKS 50000000ull   // 0.5 s of s_memrealtime (100 MHz) to find a free logit slot
-#define CAND_SLOT(i, f) (4u * 64u * (uint32_t)(193 + 8 * (i) + (f)))
-
-// A group's sum: its four terms added in id order in fp32 (the cumulative across groups is fp64); the walk
-// inside a group compares cb + each prefix of the same sum, so the group that crosses thr holds the pick.
+// A group's sum: its four terms added in id order in fp32; the walk inside a group compares the cumulative
+// plus each prefix of the same sum, so the group that crosses the threshold holds the pick.
 __device__ __forceinline__ float samp_group(const float (&q)[4]) {
     return ((q[0] + q[1]) + q[2]) + q[3];
 }
 
-// the sampled pick inside one group of four ids (base .. base + 3, logits x) from its cumulative cb: the
-// first id whose cumulative exceeds thr; its log-prob (x - m) - lse (logprobs.gather, nets.py:225)
-__device__ __forceinline__ void sample_group_walk(int base, double cb, const float (&x)[4], float cl, float m,
-                                                  float lse, double thr, int& pick, float& plp) {
-    float q[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) q[e] = samp_p(x[e], cl);
-    const float c1 = q[0] + q[1], c2 = c1 + q[2], c3 = c2 + q[3];
-    const int e = cb + (double)q[0] > thr ? 0 : cb + (double)c1 > thr ? 1 : cb + (double)c2 > thr ? 2 : 3;
-    (void)c3;
-    pick = base + e;
-    plp = (x[e] - m) - lse;
+// 2^e x for fp64 x, exact (e clamped: a term 2^-2000 below the reference is 0 anyway)
+__device__ __forceinline__ double samp_scale(double x, float e) {
+    return x == 0.0 ? 0.0 : __builtin_ldexp(x, (int)fmaxf(e, -2000.f));
 }
 
-// the row's pick from the two lanes' own picks (0x7fffffff: none): V1 - 1 if neither lane found one
-__device__ __forceinline__ void sample_settle(const DecodeParams& p, int hh, int mine, float mlp, float lastlp,
-                                              int& tok, float& lpv) {
-    const int other = __shfl_xor(mine, 32);
-    const float olp = __shfl_xor(mlp, 32), olast = __shfl_xor(lastlp, 32);
-    if (mine != 0x7fffffff) { tok = mine; lpv = mlp; }
-    else if (other != 0x7fffffff) { tok = other; lpv = olp; }
-    else { tok = p.V1 - 1; lpv = ((p.V1 - 1) & 4) >> 2 == hh ? lastlp : olast; }
-}
-
-// One chain of a stage (ids from vb, lane layout as in sample_walk_hbm): REC adds its groups to cum and keeps
-// this lane's candidate groups; the walk (REC = false) stops at the first group whose cumulative crosses thr and
-// has its lane walk the group's ids (mine / mlp)
-template <bool REC>
-__device__ __forceinline__ void sample_chain(const f32x16& acc, int vb, int hh, float cl, float m, float lse,
-                                             double thr, double lo, double hi, rsrc_t scr, uint32_t lo4,
-                                             double& cum, bool& found, int& mine, float& mlp, int& ncand) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {                        // groups (k, half 0), (k, half 1) in id order
-        float q[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) q[e] = samp_p(acc[4 * k + e], cl);
-        const double g = (double)samp_group(q);
-        const double go = __shfl_xor(g, 32);
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const bool own = half == hh;
-            const double gs = own ? g : go;
-            if (REC) {
-                // a zero group never holds the pick: the group before it would have crossed already
-                if (own && gs > 0.0 && cum <= hi && cum + gs > lo) {
-                    if (ncand < SAMPLE_NCAND) {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) st1(scr, lo4 + CAND_SLOT(ncand, e), 0u, acc[4 * k + e]);
-                        const uint64_t cbits = __builtin_bit_cast(uint64_t, cum);
-                        st1(scr, lo4 + CAND_SLOT(ncand, 4), 0u, __builtin_bit_cast(float, (uint32_t)cbits));
-                        st1(scr, lo4 + CAND_SLOT(ncand, 5), 0u, __builtin_bit_cast(float, (uint32_t)(cbits >> 32)));
-                        st1(scr, lo4 + CAND_SLOT(ncand, 6), 0u, __builtin_bit_cast(float, vb + 8 * k));
-                    }
-                    ++ncand;
-                }
-                cum += gs;
-            } else {
-                if (!found && cum + gs > thr) {
-                    found = true;
-                    if (own) {
-                        float x[4];
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) x[e] = acc[4 * k + e];
-                        sample_group_walk(vb + 8 * k, cum, x, cl, m, lse, thr, mine, mlp);
-                    }
-                }
-                if (!found) cum += gs;
-            }
-        }
-    }
-}
-
-// the log-prob of id V1 - 1 if this lane holds it in the chain from vb
-__device__ __forceinline__ void sample_last_lp(const DecodeParams& p, const f32x16& acc, int vb, float m, float lse,
-                                               float& lastlp) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if (vb + 8 * (i >> 2) + (i & 3) == p.V1 - 1) lastlp = (acc[i] - m) - lse;
-}
-
-// The sampled pick (FCModel._sample with greedy=False, nets.py:210-231; RandomState.choice: the first id whose
-// cumulative probability exceeds the draw): one pass over the logits the logit loop stored for this step
-// (LogitStore; no GEMM, no LDS, no barrier), each lane reading back its own 32 logits per stage, one stage ahead
-// of the walk, past this CU's L1. The row's cumulative sum of p (samp_p) runs in index order against
-// thr = u * sum(p), fp64 across groups of four ids (samp_group); a lane holds, per chain c, ids
-// 64s + 32c + 8k + 4hh + e (k, e < 4): the two lanes of a row exchange their group sums and step through the
-// eight groups of each chain in id order (sample_chain).
-// REC = false (the walk): tok / lpv = the pick and its log-prob; V1 - 1 if the sums never reach thr.
-// REC = true (thr unused): only the total, and each lane's candidate groups for any threshold in (lo, hi]
-// go to its scratch (scr at lane offset lo4; ncand = their count).
-// Both: the log-prob of id V1 - 1 to lastlp. Returns the row's total of p in the walk's order.
-template <bool REC>
-__device__ __forceinline__ double sample_walk_hbm(const DecodeParams& p, rsrc_t lr, uint32_t vo, int hh, float m,
-                                                  float lse, double thr, double lo, double hi, rsrc_t scr, uint32_t lo4,
-                                                  int& ncand, float& lastlp, int& tok, float& lpv) {
-    const int nst = (p.V1 + 63) >> 6;
-    const float cl = (m + lse) * LOG2E;
-    double cum = 0.0;
-    bool found = false;
-    int mine = 0x7fffffff;
-    float mlp = 0.f;
-    if (REC) ncand = 0;
-    auto load = [&](int s, f32x16& x0, f32x16& x1) __attribute__((always_inline)) {
-        const uint32_t so = SLOG_STAGE_BYTES * (uint32_t)s;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(lr, (int)vo, (int)(so + 1024u * k), 16));
-            const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(lr, (int)vo, (int)(so + 1024u * (4 + k)), 16));
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { x0[4 * k + e] = a[e]; x1[4 * k + e] = b[e]; }
-        }
-    };
-    auto walk = [&](int s, const f32x16& x0, const f32x16& x1) __attribute__((always_inline)) {
-        sample_chain<REC>(x0, 64 * s + 4 * hh, hh, cl, m, lse, thr, lo, hi, scr, lo4, cum, found, mine, mlp, ncand);
-        sample_chain<REC>(x1, 64 * s + 32 + 4 * hh, hh, cl, m, lse, thr, lo, hi, scr, lo4, cum, found, mine, mlp, ncand);
-        if (s + 1 == nst) {
-            sample_last_lp(p, x0, 64 * s + 4 * hh, m, lse, lastlp);
-            sample_last_lp(p, x1, 64 * s + 32 + 4 * hh, m, lse, lastlp);
-        }
-    };
-#if SLOG_DEPTH == 3
-    f32x16 a0, a1, b0, b1, c0, c1;
-    load(0, a0, a1);
-    load(min(1, nst - 1), b0, b1);
-    load(min(2, nst - 1), c0, c1);
-    for (int s = 0; s < nst; s += 3) {
-        walk(s, a0, a1);
-        load(min(s + 3, nst - 1), a0, a1);               // (past the end: a repeated, unused stage)
-        if (s + 1 < nst) walk(s + 1, b0, b1);
-        load(min(s + 4, nst - 1), b0, b1);
-        if (s + 2 < nst) walk(s + 2, c0, c1);
-        load(min(s + 5, nst - 1), c0, c1);
-    }
-#else
-    f32x16 a0, a1, b0, b1;
-    load(0, a0, a1);
-    load(min(1, nst - 1), b0, b1);
-    for (int s = 0; s < nst; s += 2) {
-        walk(s, a0, a1);
-        load(min(s + 2, nst - 1), a0, a1);               // (past the end: a repeated, unused stage)
-        if (s + 1 < nst) walk(s + 1, b0, b1);
-        load(min(s + 3, nst - 1), b0, b1);
-    }
-#endif
-    if (!REC) sample_settle(p, hh, mine, mlp, lastlp, tok, lpv);
-    return cum;
-}
-
-// The pick from the candidates of sample_walk_hbm<true> at thr (in (lo, hi]): the first group in id order with
-// cb + gs > thr (gs summed again from its logits as the pass summed it), walked by its lane -- the same sums,
-// so the same pick as the walking pass at thr.
-__device__ __forceinline__ void sample_pick_cand(const DecodeParams& p, int hh, rsrc_t scr, uint32_t lo4, int ncand,
-                                                 float m, float lse, float lastlp, double thr, int& tok, float& lpv) {
-    const float cl = (m + lse) * LOG2E;
-    int fb = 0x7fffffff;
-    double fcb = 0.0;
-    float fx[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int i = 0; i < ncand; ++i) {
-        float x[4], q[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            x[e] = ld1(scr, lo4 + CAND_SLOT(i, e), 0u);
-            q[e] = samp_p(x[e], cl);
-        }
-        const uint64_t cbits = (uint64_t)__builtin_bit_cast(uint32_t, ld1(scr, lo4 + CAND_SLOT(i, 4), 0u)) |
-                               ((uint64_t)__builtin_bit_cast(uint32_t, ld1(scr, lo4 + CAND_SLOT(i, 5), 0u)) << 32);
-        const double cb = __builtin_bit_cast(double, cbits);
-        const int base = __builtin_bit_cast(int, ld1(scr, lo4 + CAND_SLOT(i, 6), 0u));
-        if (cb + (double)samp_group(q) > thr) {
-            fb = base; fcb = cb;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) fx[e] = x[e];
-            break;
-        }
-    }
-    int mine = 0x7fffffff;
-    float mlp = 0.f;
-    if (fb < __shfl_xor(fb, 32)) sample_group_walk(fb, fcb, fx, cl, m, lse, thr, mine, mlp);
-    sample_settle(p, hh, mine, mlp, lastlp, tok, lpv);
-}
-
-// logit_stages hook run after each stage's epilogue with the stage's two tiles (G = 4) and its index
+// logit_stages hook run after each stage (G = 4) with the stage's two tiles and its index; `replaces`: in
+// place of the greedy epilogue
 struct NoHook {
+    static constexpr bool replaces = false;
     __device__ __forceinline__ void operator()(const f32x16&, const f32x16&, int) const {}
 };
 
-// the sampled decode's logit store: a lane's 32 logits of stage s as eight 16-byte words, word k of lane l of
-// wave w at byte s * 64 KiB + w * 8 KiB + k * 1 KiB + 16 l of the workgroup's slot (one wave instruction
-// writes 1 KiB contiguous); the walk (sample_walk_hbm) reads them back in the same lane
-struct LogitStore {
-    rsrc_t r;
-    uint32_t vo;      // 16 * lane + 8192 * wave
+// the sampled decode's logit loop epilogue: running max m, reference r = ceil(m log2e), the lane's running sum T
+// of its terms relative to 2^r; stores the stage's logits and {P, r} to the slot (one wave instruction per
+// 1 KiB word)
+struct SampleStage {
+    static constexpr bool replaces = true;
+    rsrc_t slot;
+    uint32_t vo;      // 16 * lane + SLOG_WAVE_BYTES * wave
+    float& m;
+    float& ref;
+    double& T;
     __device__ __forceinline__ void operator()(const f32x16& q0, const f32x16& q1, int s) const {
         if (s < 0) return;                               // the pipeline's first epilogue: no stage yet
         const uint32_t so = SLOG_STAGE_BYTES * (uint32_t)s;
@@ -965,11 +791,176 @@ struct LogitStore {
         for (int k = 0; k < 4; ++k) {
             const f32x4 a = {q0[4 * k], q0[4 * k + 1], q0[4 * k + 2], q0[4 * k + 3]};
             const f32x4 b = {q1[4 * k], q1[4 * k + 1], q1[4 * k + 2], q1[4 * k + 3]};
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), r, (int)vo, (int)(so + 1024u * k), 0);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), r, (int)vo, (int)(so + 1024u * (4 + k)), 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), slot, (int)vo, (int)(so + 1024u * k), 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), slot, (int)vo, (int)(so + 1024u * (4 + k)), 0);
         }
+        const float mnew = vmax2(m, vmax2(vmax16(q0), vmax16(q1)));
+        const float rnew = ceilf(mnew * LOG2E);
+        if (rnew > ref) {
+            T = samp_scale(T, ref - rnew);
+            ref = rnew;
+        }
+        m = mnew;
+        double P = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float qa[4], qb[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                qa[e] = samp_p(q0[4 * k + e], ref);
+                qb[e] = samp_p(q1[4 * k + e], ref);
+            }
+            P += (double)samp_group(qa);
+            P += (double)samp_group(qb);
+        }
+        T += P;
+        const uint64_t pb = __builtin_bit_cast(uint64_t, P);
+        const u32x4 w = {(uint32_t)pb, (uint32_t)(pb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
+        __builtin_amdgcn_raw_buffer_store_b128(w, slot, (int)vo, (int)(so + 8u * 1024u), 0);
     }
 };
+
+// The walk over one stage's logits (x0 / x1: the lane's chains a / b; ids 64s + 32c + 8k + 4hh + e) from the
+// cumulative cb, the lane's terms scaled by sc = 2^(r - R): the first group in id order (the two lanes of a row
+// alternate) whose cumulative exceeds thr, then its first id. mine / mlp: the pick and its log-prob
+// (logprobs.gather, nets.py:225) on the lane holding it; found stays false if the stage's sums stop short.
+__device__ __forceinline__ void sample_stage_walk(const f32x16& x0, const f32x16& x1, int s, int hh, float ref,
+                                                  double sc, float m, float lse, double thr, double& cb, bool& found,
+                                                  int& mine, float& mlp) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float x[4], q[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                x[e] = c ? x1[4 * k + e] : x0[4 * k + e];
+                q[e] = samp_p(x[e], ref);
+            }
+            const float c1 = q[0] + q[1], c2 = c1 + q[2], g = c2 + q[3];
+            const double gs = (double)g * sc;
+            const double go = __shfl_xor(gs, 32);
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const bool own = half == hh;
+                const double gv = own ? gs : go;
+                if (!found && cb + gv > thr) {
+                    found = true;
+                    if (own) {
+                        const int e = cb + (double)q[0] * sc > thr ? 0 : cb + (double)c1 * sc > thr ? 1
+                                    : cb + (double)c2 * sc > thr ? 2 : 3;
+                        mine = 64 * s + 32 * c + 8 * k + 4 * hh + e;
+                        mlp = (x[e] - m) - lse;
+                    }
+                }
+                if (!found) cb += gv;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void samp_load_stage(rsrc_t lr, uint32_t vo, uint32_t so, f32x16& x0, f32x16& x1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(lr, (int)(vo + so), (int)(1024u * k), 16));
+        const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(lr, (int)(vo + so), (int)(1024u * (4 + k)), 16));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { x0[4 * k + e] = a[e]; x1[4 * k + e] = b[e]; }
+    }
+}
+
+// The pick of each row from its stored step (lr: the workgroup's slot, vo: the lane's offset in it), R: the row's
+// common reference, thr = u * T. FULL (test hook NICNES_FORCE_EXACT): the walk runs through every stage's
+// logits instead of scanning the stage sums first (the same terms; the sums associate differently, ~1e-16).
+// If the crossing stage's own sums stop short of thr (rounding) or no stage crosses, the pick is the last id of
+// that stage / V1 - 1 (stats[1] counts those rows).
+template <bool FULL>
+__device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, uint32_t vo, int hh, float m, float lse,
+                                            float R, double thr, int& tok, float& lpv) {
+    const int nst = (p.V1 + 63) >> 6;
+    double cum = 0.0, cb = 0.0;
+    bool found = false;
+    int mine = 0x7fffffff;
+    float mlp = 0.f;
+    int sf = nst - 1;                                    // the stage whose sums cross thr (default: the last)
+    float rf = 0.f;
+    if constexpr (FULL) {
+        for (int s = 0; s < nst; ++s) {
+            const f32x4 w = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(lr, (int)vo, (int)(SLOG_STAGE_BYTES * s + 8u * 1024u), 16));
+            f32x16 x0, x1;
+            samp_load_stage(lr, vo, SLOG_STAGE_BYTES * (uint32_t)s, x0, x1);
+            const double c0 = cum;
+            sample_stage_walk(x0, x1, s, hh, w[2], __builtin_ldexp(1.0, (int)fmaxf(w[2] - R, -2000.f)), m, lse, thr, cum,
+                              found, mine, mlp);
+            if (!found) { sf = s; cb = c0; rf = w[2]; }  // (kept for the no-crossing case: the last stage)
+        }
+        if (found) sf = -1;
+    } else {
+        bool have = false;
+        double cl = 0.0;
+        float rl = 0.f;
+        for (int s0 = 0; s0 < nst; s0 += 8) {
+            f32x4 w[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                w[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(lr, (int)vo, (int)(SLOG_STAGE_BYTES * min(s0 + j, nst - 1) + 8u * 1024u), 16));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (s0 + j < nst) {
+                    const double P = __builtin_bit_cast(double, (uint64_t)__builtin_bit_cast(uint32_t, w[j][0]) |
+                                                                ((uint64_t)__builtin_bit_cast(uint32_t, w[j][1]) << 32));
+                    const double a = samp_scale(P, w[j][2] - R);
+                    const double ao = __shfl_xor(a, 32);
+                    const double S = hh == 0 ? a + ao : ao + a;
+                    if (!have) {
+                        if (cum + S > thr) { have = true; sf = s0 + j; cb = cum; rf = w[j][2]; }
+                        else { cl = cum; rl = w[j][2]; cum += S; }
+                    }
+                }
+            }
+            if (__all(have ? 1 : 0)) break;
+        }
+        if (!have) { sf = nst - 1; cb = cl; rf = rl; }
+        f32x16 x0, x1;
+        samp_load_stage(lr, vo, SLOG_STAGE_BYTES * (uint32_t)sf, x0, x1);
+        sample_stage_walk(x0, x1, sf, hh, rf, __builtin_ldexp(1.0, (int)fmaxf(rf - R, -2000.f)), m, lse, thr, cb, found,
+                          mine, mlp);
+        if (found) sf = -1;
+        else {                                           // the stage's sums stop short: its last id
+            const int id = min(64 * sf + 63, p.V1 - 1), j = id - 64 * sf, jj = j & 31;
+            if (((jj >> 2) & 1) == hh) {
+                float xv = 0.f;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (4 * (jj >> 3) + (jj & 3) == i) xv = (j >> 5) ? x1[i] : x0[i];
+                }
+                mine = id;
+                mlp = (xv - m) - lse;
+            }
+        }
+    }
+    if constexpr (FULL) {
+        if (sf >= 0) {                                   // no stage crossed: V1 - 1, from the last stage
+            f32x16 x0, x1;
+            samp_load_stage(lr, vo, SLOG_STAGE_BYTES * (uint32_t)(nst - 1), x0, x1);
+            const int id = p.V1 - 1, j = id - 64 * (nst - 1), jj = j & 31;
+            if (((jj >> 2) & 1) == hh) {
+                float xv = 0.f;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (4 * (jj >> 3) + (jj & 3) == i) xv = (j >> 5) ? x1[i] : x0[i];
+                }
+                mine = id;
+                mlp = (xv - m) - lse;
+            }
+        }
+    }
+    if (sf >= 0 && hh == 0) atomicAdd(p.stats + 1, 1);
+    const int other = __shfl_xor(mine, 32);
+    const float olp = __shfl_xor(mlp, 32);
+    if (mine != 0x7fffffff) { tok = mine; lpv = mlp; }
+    else { tok = other; lpv = olp; }
+}
 
 template <int G, bool PAIRS, class Tail = NoTail, class Hook = NoHook>
 __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, uint64_t nidx, int wave, int sgn,
@@ -1028,13 +1019,13 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
             if (sgn == MFMA_FIRST_SIGN) {
                 mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
 #if !(DECODE_ABLATE & 1)
-                epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
-                hook(q0, q1, s - 1);
+                if constexpr (Hook::replaces) hook(q0, q1, s - 1);
+                else epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
 #endif
             } else {
 #if !(DECODE_ABLATE & 1)
-                epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
-                hook(q0, q1, s - 1);
+                if constexpr (Hook::replaces) hook(q0, q1, s - 1);
+                else epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
 #endif
                 mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
             }
@@ -1058,8 +1049,8 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
     };
     auto last = [&](const f32x16& q0, const f32x16& q1, int s) {
         if constexpr (G == 4) {
-            epilogue64<PAIRS>(st, q0, q1, 64 * s + vl);
-            hook(q0, q1, s);
+            if constexpr (Hook::replaces) hook(q0, q1, s);
+            else epilogue64<PAIRS>(st, q0, q1, 64 * s + vl);
         } else {
             epilogue32<PAIRS>(st, q0, 64 * s + vl);
         }
@@ -1334,8 +1325,8 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img64_kernel(DecodePar
 // one step of one workgroup; false when the workgroup is done (every row finished, or t = T).
 // s64 / pre (the steps kernel): staging registers kept across steps; pre says they hold this step's first
 // logit tile, loaded during the previous step's last cell stage (PREFETCH: that load is issued)
-// SAMPLE: the sampled decode (nets.py:210-231): the logit loop keeps only the exact (m, exp-sum), then
-// sample_walk_hbm picks each row's token from its draw p.sample_u over the logits the loop stored (fused path only)
+// SAMPLE: the sampled decode (nets.py:210-231): the logit loop stores its logits and stage sums (SampleStage), then
+// sample_pick draws each row's token with its uniform p.sample_u (fused path only)
 template <bool PAIRS, bool PREFETCH, bool SAMPLE = false>
 __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, float* lds, int t, Stage64Regs& s64,
                                           bool& pre, float (&hB)[64], bool& hpre) {
@@ -1379,9 +1370,12 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         auto tail = [&]() __attribute__((always_inline)) {
             if (xpre) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
         };
-        if constexpr (SAMPLE) {                                  // the logits also go to the workgroup's slot
-            const LogitStore ls{c.slog_r, 16u * (uint32_t)lane_fresh() + 8192u * (uint32_t)c.wave};
-            logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail, ls);
+        // SAMPLE: the lane's running max, reference and sum of terms (SampleStage), the logits to the slot
+        float sm = -1.0e30f, sref = -1.0e30f;
+        double sT = 0.0;
+        if constexpr (SAMPLE) {
+            const SampleStage ss{c.slog_r, 16u * (uint32_t)lane_fresh() + SLOG_WAVE_BYTES * (uint32_t)c.wave, sm, sref, sT};
+            logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail, ss);
         } else {
             logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail);
         }
@@ -1401,28 +1395,18 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         if constexpr (SAMPLE) {
             const size_t ou = (((size_t)c.member * 2 + c.sgn) * p.B + c.bc) * p.T + (t - 1);
             const double u = c.row_valid ? p.sample_u[ou] : 0.5;
-            // thr = u * the row's sum of p, summed exactly as the walk sums (the pass-1 exp-sum stot differs from
-            // it by ~1e-6: its exponents carry the rounding of m * log2e). One pass sums it and keeps the groups
-            // that can hold the pick for any thr within SAMPLE_BAND of u * stot e^-lse; a row whose thr falls
-            // outside (or with more candidates than kept) sends its wave through a second, walking pass.
-            const double test = (double)stot * exp(-(double)lse);
-            const double blo = u * test * (1.0 - SAMPLE_BAND), bhi = u * test * (1.0 + SAMPLE_BAND);
-            int ncand = 0;
-            float lastlp = 0.f;
-            // the logit loop stored this step's logits: the passes read them back, each wave on its own (a wave
-            // whose threshold misses walks again, alone)
-            const uint32_t vo = 16u * (uint32_t)c.lane + 8192u * (uint32_t)c.wave;
-            const double tot = sample_walk_hbm<true>(p, c.slog_r, vo, c.hh, m, lse, 0.0, blo, bhi, c.scr_r, lo, ncand,
-                                                     lastlp, tok, lp_tok);
-            const double thr = u * tot;
-            const bool miss = !(thr > blo && thr <= bhi) || ncand > SAMPLE_NCAND;
-            if (__any((miss || p.force_exact) ? 1 : 0)) {
-                sample_walk_hbm<false>(p, c.slog_r, vo, c.hh, m, lse, thr, blo, bhi, c.scr_r, lo, ncand, lastlp, tok,
-                                       lp_tok);
-                if (c.lane == 0) atomicAdd(p.stats + 1, 1);
-            } else {
-                sample_pick_cand(p, c.hh, c.scr_r, lo, ncand, m, lse, lastlp, thr, tok, lp_tok);
-            }
+            // the row: max, common reference R, sum T of its terms relative to 2^R (lane 0's part first), lse
+            const float mo = __shfl_xor(sm, 32), ro = __shfl_xor(sref, 32);
+            const double To = __shfl_xor(sT, 32);
+            const float mr = fmaxf(sm, mo), R = fmaxf(sref, ro);
+            const double ta = samp_scale(sT, sref - R), tb = samp_scale(To, ro - R);
+            const double T = c.hh == 0 ? ta + tb : tb + ta;
+            const float lse_s = (float)(log(T) + (double)R * 0.69314718055994531 - (double)mr);
+            const uint32_t vo = 16u * (uint32_t)c.lane + SLOG_WAVE_BYTES * (uint32_t)c.wave;
+            if (p.force_exact)
+                sample_pick<true>(p, c.slog_r, vo, c.hh, mr, lse_s, R, u * T, tok, lp_tok);
+            else
+                sample_pick<false>(p, c.slog_r, vo, c.hh, mr, lse_s, R, u * T, tok, lp_tok);
         } else {
             const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
             const int ci[4] = {st.r0i, st.r1i, __shfl_xor(st.r0i, 32), __shfl_xor(st.r1i, 32)};
@@ -1625,6 +1609,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodePar
         if (slot < 0) return;
         const int nst = (p.V1 + 63) >> 6;
         c.slog_r = make_rsrc(p.slog + (size_t)slot * nst * (SLOG_STAGE_BYTES / 4), SLOG_STAGE_BYTES * (uint32_t)nst);
+        static_assert(SLOG_STAGE_BYTES % 4 == 0, "slot stage size");
     }
     wave_prio(c.wave);
     Stage64Regs s64;

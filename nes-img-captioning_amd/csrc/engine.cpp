@@ -864,9 +864,9 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
         p.sample_u = h->su;
         if (!h->slog) {
             // a slot per resident workgroup (one per CU: the steps kernel's LDS) plus spares, each holding one
-            // step's logits of a workgroup's 2 x 128 rows (nst stages of 64 KiB)
+            // step's logits and stage sums of a workgroup's 2 x 128 rows (nst stages of 72 KiB)
             const int ns = h->test_slots > 0 ? h->test_slots : h->sample_occ * h->n_cu + 16;
-            const size_t per = (size_t)((h->V1 + 63) / 64) * 16384;
+            const size_t per = (size_t)((h->V1 + 63) / 64) * 18432;   // 72 KiB per stage (decode_kernel.hip)
             HIPC(h, hipDeviceSynchronize());
             int rc = dalloc(h, &h->slog, per * ns);
             if (!rc) rc = dalloc(h, &h->slog_slots, (size_t)ns);

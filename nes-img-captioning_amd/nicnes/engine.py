@@ -424,5 +424,5 @@ class Engine:
     def stats(self):
         out = (ctypes.c_int64 * 4)()
         check(self.L.nicnes_stats(self.h, out), self.h, 'stats')
-        return {'tie_fallbacks': out[0], 'sample_resweeps': out[1], 'coop_timeouts': out[2],
+        return {'tie_fallbacks': out[0], 'sample_stage_fallbacks': out[1], 'coop_timeouts': out[2],
                 'sample_slot_timeouts': out[3]}
