@@ -900,21 +900,26 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
         double cl = 0.0;
         float rl = 0.f;
         for (int s0 = 0; s0 < nst; s0 += 8) {
-            f32x4 w[8];
+            // P and r as their own loads (a 16-byte load narrowed by the compiler returned P's low word as r)
+            double Pw[8];
+            float rw[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                w[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(lr, (int)vo, (int)(SLOG_STAGE_BYTES * min(s0 + j, nst - 1) + 8u * 1024u), 16));
+            for (int j = 0; j < 8; ++j) {
+                const int so = (int)(SLOG_STAGE_BYTES * min(s0 + j, nst - 1) + 8u * 1024u);
+                Pw[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lr, (int)vo, so, 16));
+                rw[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (int)vo + 8, so, 16));
+            }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if (s0 + j < nst) {
-                    const double P = __builtin_bit_cast(double, (uint64_t)__builtin_bit_cast(uint32_t, w[j][0]) |
-                                                                ((uint64_t)__builtin_bit_cast(uint32_t, w[j][1]) << 32));
-                    const double a = samp_scale(P, w[j][2] - R);
+                    const double P = Pw[j];
+                    const float r = rw[j];
+                    const double a = samp_scale(P, r - R);
                     const double ao = __shfl_xor(a, 32);
                     const double S = hh == 0 ? a + ao : ao + a;
                     if (!have) {
-                        if (cum + S > thr) { have = true; sf = s0 + j; cb = cum; rf = w[j][2]; }
-                        else { cl = cum; rl = w[j][2]; cum += S; }
+                        if (cum + S > thr) { have = true; sf = s0 + j; cb = cum; rf = r; }
+                        else { cl = cum; rl = r; cum += S; }
                     }
                 }
             }
