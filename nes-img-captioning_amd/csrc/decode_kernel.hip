@@ -47,7 +47,8 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef DECODE_ABLATE
 #define DECODE_ABLATE 0    // timing-only builds (scripts/ablate.py): 1 no logit epilogue, 4 no exp-sum, 2 no stage
 #endif                     // staging, 8 no stage-loop barrier, 16 no cell activations, 64 no early
-                           // exit, 128 no coop hand-off waits -- wrong results
+                           // exit, 128 no coop hand-off waits, 256 no sampled logit stores, 512 no sampled
+                           // pick -- wrong results
 #if DECODE_ABLATE & 16
 #define CELL_SIG(x) ((x) * 0.5f)
 #define CELL_TANH(x) ((x) * 0.25f)
@@ -751,6 +752,9 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
 #define SLOG_WAVE_BYTES 9216u                  // 9 words x 64 lanes x 16 bytes
 #define SLOG_STAGE_BYTES (8u * SLOG_WAVE_BYTES)  // one 64-row stage of a workgroup (72 KiB)
 #define SLOT_SPIN_TICKS 50000000ull   // 0.5 s of s_memrealtime (100 MHz) to find a free logit slot
+#ifndef SLOG_STORE_POLICY
+#define SLOG_STORE_POLICY 0      // cache policy of the slot stores (2: nt, streaming past the L2's normal allocation)
+#endif
 
 __device__ __forceinline__ float samp_p(float x, float ref) {
     return __builtin_amdgcn_exp2f(__builtin_fmaf(x, LOG2E, -ref));
@@ -787,13 +791,15 @@ struct SampleStage {
     __device__ __forceinline__ void operator()(const f32x16& q0, const f32x16& q1, int s) const {
         if (s < 0) return;                               // the pipeline's first epilogue: no stage yet
         const uint32_t so = SLOG_STAGE_BYTES * (uint32_t)s;
+#if !(DECODE_ABLATE & 256)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const f32x4 a = {q0[4 * k], q0[4 * k + 1], q0[4 * k + 2], q0[4 * k + 3]};
             const f32x4 b = {q1[4 * k], q1[4 * k + 1], q1[4 * k + 2], q1[4 * k + 3]};
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), slot, (int)vo, (int)(so + 1024u * k), 0);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), slot, (int)vo, (int)(so + 1024u * (4 + k)), 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), slot, (int)vo, (int)(so + 1024u * k), SLOG_STORE_POLICY);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), slot, (int)vo, (int)(so + 1024u * (4 + k)), SLOG_STORE_POLICY);
         }
+#endif
         const float mnew = vmax2(m, vmax2(vmax16(q0), vmax16(q1)));
         const float rnew = ceilf(mnew * LOG2E);
         if (rnew > ref) {
@@ -816,7 +822,7 @@ struct SampleStage {
         T += P;
         const uint64_t pb = __builtin_bit_cast(uint64_t, P);
         const u32x4 w = {(uint32_t)pb, (uint32_t)(pb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
-        __builtin_amdgcn_raw_buffer_store_b128(w, slot, (int)vo, (int)(so + 8u * 1024u), 0);
+        __builtin_amdgcn_raw_buffer_store_b128(w, slot, (int)vo, (int)(so + 8u * 1024u), SLOG_STORE_POLICY);
     }
 };
 
@@ -1408,10 +1414,15 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
             const double T = c.hh == 0 ? ta + tb : tb + ta;
             const float lse_s = (float)(log(T) + (double)R * 0.69314718055994531 - (double)mr);
             const uint32_t vo = 16u * (uint32_t)c.lane + SLOG_WAVE_BYTES * (uint32_t)c.wave;
+#if DECODE_ABLATE & 512
+            tok = 1 + (int)(u * 9000.0);                 // timing only: no pick
+            lp_tok = -lse_s;
+#else
             if (p.force_exact)
                 sample_pick<true>(p, c.slog_r, vo, c.hh, mr, lse_s, R, u * T, tok, lp_tok);
             else
                 sample_pick<false>(p, c.slog_r, vo, c.hh, mr, lse_s, R, u * T, tok, lp_tok);
+#endif
         } else {
             const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
             const int ci[4] = {st.r0i, st.r1i, __shfl_xor(st.r0i, 32), __shfl_xor(st.r1i, 32)};

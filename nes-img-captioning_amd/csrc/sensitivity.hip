@@ -1,30 +1,179 @@
-// sensitivity.hip -- the SM-G-SUM sensitivity of safe mutations on the GPU.
+// sensitivity.hip -- the SM-G-SUM sensitivity of safe mutations on the GPU, hand-written MFMA kernels.
 //
 // Replaces the per-task host computation of
-//   Sensitivity._calc_sum_sensitivity (/root/reference/src/algorithm/safe_mutations.py:86-110) on
+//   Sensitivity._calc_sum_sensitivity (/root/reference/src/algorithm/safe_mutations.py:93-117) on
 //   CaptionModel.forward_for_sensitivity (/root/reference/src/captioning/nets.py:22-70):
 // O = [Bs, K] grouped log-prob norms after L = 5 greedy steps (vocabulary zero-padded to a multiple of
 // split = 100, K groups, each reduced to its 2-norm); the reference runs K backward passes, one per
-// column k of O summed over the batch, and returns s_j = sqrt(sum_k (dO_k / dtheta_j)^2) / Bs.
+// column k of O summed over the batch, stacks the K gradients into a [K, D] Jacobian J and returns
+// s_j = sqrt(sum_k J[k, j]^2) / Bs (safe_mutations.py:112-117).
 //
-// Here the K backward passes run at once: the K output seeds dZ_k = d(sum_b O[b, k]) / d logits are
-// formed in one kernel, and every backward product is one strided-batched GEMM over k (rocBLAS, fp32:
-// plain library GEMMs), with the per-k gradients G[k, :] laid out in the flat theta order;
-// one last pass reduces sqrt(sum_k G[k, j]^2) / Bs and applies the clamp of calc_sensitivity
-// (safe_mutations.py:63-65). The greedy tokens of the forward come from the engine's bit-exact decode
-// (unmasked, as forward_for_sensitivity feeds argmax back without the finished mask); the forward
-// activations the backward needs are recomputed here in fp32. Agreement with the reference's vector is
-// to a stated tolerance (fp32 sums in another order), not bit for bit.
+// Here the K backward passes run at once and the Jacobian is never written: every weight gradient is a
+// product G_k = A_k^T B over the batch (and the cells), and sq_tile (below) forms G_k tile by tile on
+// fp32 MFMA and adds G_k^2 into its registers, k after k; only sum_k G_k^2 leaves the kernel (a few
+// k-range partials, summed in a fixed order by sens_finish). The plain products of the forward and of
+// the backward recurrence run on the same tile kernel (gemm mode). Structure used:
+//   * the output seed of group k, dZ_k = d(sum_b O[b, k]) / d logits, is own_k - p * S_k (sens_seed):
+//     own_k nonzero only inside group k. The logit.weight factor reads dZ from (lp, p, inv_g, S) as it
+//     stages it (DzA, nothing [K, Bs, V] is stored), and dH_L = dZ_k Wl is inv_g (lp Wl restricted to
+//     the group) - S_k (p Wl): one [Bs, V] x [V, R] product instead of K of them (sens_dh_logit);
+//   * the embedding rows gather dX of the cells whose token is that row: a deterministic per-token sum
+//     (sens_emb_sq), no atomics, so the vector is the same in every process.
+// The greedy tokens of the forward come from the engine's bit-exact decode (unmasked, as
+// forward_for_sensitivity feeds argmax back without the finished mask); the forward activations are
+// recomputed here in fp32. Agreement with the reference's vector is to a stated tolerance (fp32 sums in
+// another order), not bit for bit.
 #include <hip/hip_runtime.h>
-#include <rocblas/rocblas.h>
 #include <stdint.h>
 
 #include "sensitivity.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
+// ---- the tile kernel -----------------------------------------------------------------------------
+// C[m, n] = sum_r A(k, m, r) B(k, r, n) over a 64 x 64 tile per workgroup of 4 waves (wave w: rows
+// 32 (w >> 1), columns 32 (w & 1) of the tile, one v_mfma_f32_32x32x2_f32 accumulator), the reduction
+// staged through LDS in chunks of 16, the next chunk's global loads issued before this chunk's MFMAs.
+// gemm mode: k = blockIdx.z (a batch), C written (beta 0) or accumulated (beta 1).
+// sq mode: k runs over [k0, k1) of range blockIdx.z, C_k is formed for each k and C_k^2 accumulated;
+// out[z][m, n] = sum over the range (sq partials, summed over ranges by sens_finish).
+#define TM 64
+#define TN 64
+#define TR 16
+#define LDS_P (TM + 1)
+
+struct Strided {             // element (k, m, r) at p + k sk + m sm + r sr
+    const float* p;
+    int64_t sk, sm, sr;
+    __device__ __forceinline__ float operator()(int k, int m, int r) const {
+        return p[(int64_t)k * sk + (int64_t)m * sm + (int64_t)r * sr];
+    }
+    __device__ __forceinline__ bool m_unit() const { return sm == 1; }
+};
+
+// dZ_k[b, v] = [v in group k] lp[b, v] inv_g[b, k] - p[b, v] S[b, k] as A(k, m = v, r = b) (sens_seed's seed)
+struct DzA {
+    const float* lp;         // [Bs, V]
+    const float* pr;         // [Bs, V] exp(lp)
+    const float* ig;         // [Bs, K] 1 / |lp group k| (0 for an all-padding group)
+    const float* S;          // [Bs, K] sum over group k of lp inv_g
+    int V, K, split;
+    __device__ __forceinline__ float operator()(int k, int v, int b) const {
+        const int64_t o = (int64_t)b * V + v;
+        const float own = (v / split == k) ? lp[o] * ig[b * K + k] : 0.f;
+        return own - pr[o] * S[b * K + k];
+    }
+    __device__ __forceinline__ bool m_unit() const { return true; }
+};
+
+struct TileArgs {
+    int M, N, R;             // tile problem: C [M, N], reduction R
+    const float* B;          // element (k, r, n) at B + k sBk + r sBr + n sBn
+    int64_t sBk, sBr, sBn;
+    float* C;                // gemm: (k, m, n) at C + k sCk + m sCm + n sCn; sq: out + z sCk + m sCm + n sCn
+    int64_t sCk, sCm, sCn;
+    int beta;                // gemm: 1 accumulate into C
+    int k0, kpr, k_end;      // sq: range z covers k in [k0 + z kpr, min(k0 + (z + 1) kpr, k_end))
+};
+
+// chunk [r0, r0 + TR) of A (TM rows from m0) and B (TN columns from n0) into registers: 4 + 4 values per
+// thread, the 256 threads laid along the operand's unit-stride dimension
+template <class AOp>
+__device__ __forceinline__ void tile_load(const AOp& A, const TileArgs& t, int k, int m0, int n0, int r0, float (&ra)[4],
+                                          float (&rb)[4]) {
+    const int tid = threadIdx.x;
+    const bool am = A.m_unit();
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int i = tid + 256 * e;
+        const int m = am ? (i & (TM - 1)) : (i >> 4), r = am ? (i >> 6) : (i & (TR - 1));
+        const int gm = m0 + m, gr = r0 + r;
+        ra[e] = (gm < t.M && gr < t.R) ? A(k, gm, gr) : 0.f;
+    }
+    const bool bn = t.sBn == 1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int i = tid + 256 * e;
+        const int n = bn ? (i & (TN - 1)) : (i >> 4), r = bn ? (i >> 6) : (i & (TR - 1));
+        const int gn = n0 + n, gr = r0 + r;
+        rb[e] = (gn < t.N && gr < t.R) ? t.B[(int64_t)k * t.sBk + (int64_t)gr * t.sBr + (int64_t)gn * t.sBn] : 0.f;
+    }
+}
+
+template <class AOp>
+__device__ __forceinline__ void tile_store(const AOp& A, const TileArgs& t, float* As, float* Bs, const float (&ra)[4],
+                                           const float (&rb)[4]) {
+    const int tid = threadIdx.x;
+    const bool am = A.m_unit(), bn = t.sBn == 1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int i = tid + 256 * e;
+        const int m = am ? (i & (TM - 1)) : (i >> 4), r = am ? (i >> 6) : (i & (TR - 1));
+        As[r * LDS_P + m] = ra[e];
+        const int n = bn ? (i & (TN - 1)) : (i >> 4), rr = bn ? (i >> 6) : (i & (TR - 1));
+        Bs[rr * LDS_P + n] = rb[e];
+    }
+}
+
+// acc += A(k)[tile rows, :] B(k)[:, tile columns] for this wave's 32 x 32 block
+template <class AOp>
+__device__ __forceinline__ void tile_product(const AOp& A, const TileArgs& t, int k, int m0, int n0, float* As, float* Bs,
+                                             f32x16& acc) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wm = 32 * (w >> 1), wn = 32 * (w & 1), kh = lane >> 5, li = lane & 31;
+    float ra[4], rb[4];
+    tile_load(A, t, k, m0, n0, 0, ra, rb);
+    for (int r0 = 0; r0 < t.R; r0 += TR) {
+        __syncthreads();                                     // the previous chunk has been read
+        tile_store(A, t, As, Bs, ra, rb);
+        __syncthreads();
+        if (r0 + TR < t.R) tile_load(A, t, k, m0, n0, r0 + TR, ra, rb);
+#pragma unroll
+        for (int j = 0; j < TR / 2; ++j) {
+            const float a = As[(2 * j + kh) * LDS_P + wm + li];
+            const float b = Bs[(2 * j + kh) * LDS_P + wn + li];
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        }
+    }
+}
+
+template <class AOp, bool SQ>
+__global__ __launch_bounds__(256) void sens_tile(AOp A, TileArgs t) {
+    __shared__ float As[TR * LDS_P], Bs[TR * LDS_P];
+    const int m0 = blockIdx.x * TM, n0 = blockIdx.y * TN, z = blockIdx.z;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wm = 32 * (w >> 1), wn = 32 * (w & 1), kh = lane >> 5, li = lane & 31;
+    f32x16 acc, sq;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sq[i] = 0.f;
+    const int ka = SQ ? t.k0 + z * t.kpr : z, kb = SQ ? min(ka + t.kpr, t.k_end) : z + 1;
+    for (int k = ka; k < kb; ++k) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+        tile_product(A, t, k, m0, n0, As, Bs, acc);
+        if (SQ) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sq[i] += acc[i] * acc[i];
+        }
+    }
+    // accumulator element i of lane l: row 8 (i >> 2) + 4 (l >> 5) + (i & 3), column l & 31
+    const int n = n0 + wn + li;
+    if (n >= t.N) return;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int m = m0 + wm + 8 * (i >> 2) + 4 * kh + (i & 3);
+        if (m >= t.M) continue;
+        float* c = t.C + (int64_t)z * t.sCk + (int64_t)m * t.sCm + (int64_t)n * t.sCn;
+        if (SQ) *c = sq[i];
+        else *c = t.beta ? *c + acc[i] : acc[i];
+    }
+}
+
+// ---- elementwise and small kernels ------------------------------------------------------------------
 // Y[r, c] += b1[c] (+ b2[c])
 __global__ void sens_bias_rows(float* Y, const float* b1, const float* b2, int rows, int cols) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -55,11 +204,12 @@ __global__ void sens_cell_fwd(const float* S, const float* Cprev, float* C, floa
     H[i] = og * tanhf(c);
 }
 
-// one block per row: LP = log_softmax(Z) (nets.py:202)
-__global__ void sens_logsoftmax(const float* Z, float* LP, int V) {
+// one block per row: LP = log_softmax(Z) (nets.py:202), P = exp(LP)
+__global__ void sens_logsoftmax(const float* Z, float* LP, float* P, int V) {
     __shared__ float red[256];
     const float* z = Z + (int64_t)blockIdx.x * V;
     float* lp = LP + (int64_t)blockIdx.x * V;
+    float* pr = P + (int64_t)blockIdx.x * V;
     float m = -INFINITY;
     for (int v = threadIdx.x; v < V; v += blockDim.x) m = fmaxf(m, z[v]);
     red[threadIdx.x] = m;
@@ -79,12 +229,17 @@ __global__ void sens_logsoftmax(const float* Z, float* LP, int V) {
         __syncthreads();
     }
     const float lse = logf(red[0]);
-    for (int v = threadIdx.x; v < V; v += blockDim.x) lp[v] = (z[v] - m) - lse;
+    for (int v = threadIdx.x; v < V; v += blockDim.x) {
+        const float l = (z[v] - m) - lse;
+        lp[v] = l;
+        pr[v] = expf(l);
+    }
 }
 
-// block (b, k): the seed of output column k for row b through the 2-norm and log_softmax:
-// dZ[k, b, v] = [v in group k] lp[b, v] / g_bk - exp(lp[b, v]) * sum_{u in group k} lp[b, u] / g_bk
-__global__ void sens_seed(const float* LP, float* dZ, int Bs, int V, int split) {
+// block (b, k): the seed of output column k for row b through the 2-norm and log_softmax,
+// dZ[k, b, v] = [v in group k] lp[b, v] / g_bk - exp(lp[b, v]) * sum_{u in group k} lp[b, u] / g_bk,
+// kept as inv_g[b, k] = 1 / g_bk (0 for an all-padding group) and S[b, k] (DzA forms dZ from them)
+__global__ void sens_seed(const float* LP, float* IG, float* Sg, int Bs, int V, int K, int split) {
     __shared__ float red[2][128];
     const int b = blockIdx.x, k = blockIdx.y;
     const float* lp = LP + (int64_t)b * V;
@@ -105,41 +260,37 @@ __global__ void sens_seed(const float* LP, float* dZ, int Bs, int V, int split) 
         }
         __syncthreads();
     }
-    const float g = sqrtf(red[0][0]);
-    const float inv = g > 0.f ? 1.f / g : 0.f;                   // an all-padding group: no gradient
-    const float S = red[1][0] * inv;
-    float* d = dZ + ((int64_t)k * Bs + b) * V;
-    for (int v = threadIdx.x; v < V; v += blockDim.x) {
-        const float own = (v >= v0 && v < v0 + split) ? lp[v] * inv : 0.f;
-        d[v] = own - expf(lp[v]) * S;
+    if (threadIdx.x == 0) {
+        const float g = sqrtf(red[0][0]);
+        const float inv = g > 0.f ? 1.f / g : 0.f;
+        IG[b * K + k] = inv;
+        Sg[b * K + k] = red[1][0] * inv;
     }
 }
 
-// out[k][c] (+)= sum_r X[k][r][c], optionally into a second destination too
-__global__ void sens_colsum(const float* X, int rows, int cols, int64_t sX, float* out, float* out2, int64_t sO,
-                            int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x, k = blockIdx.y;
-    if (c >= cols) return;
-    const float* x = X + (int64_t)k * sX + c;
-    float s = 0.f;
-    for (int r = 0; r < rows; ++r) s += x[(int64_t)r * cols];
-    float* o = out + (int64_t)k * sO + c;
-    *o = accumulate ? *o + s : s;
-    if (out2) {
-        float* o2 = out2 + (int64_t)k * sO + c;
-        *o2 = accumulate ? *o2 + s : s;
-    }
+// dH_L[k, b, r] = sum_v dZ[k, b, v] Wl[v, r] = inv_g[b, k] sum_{v in group k} lp[b, v] Wl[v, r] - S[b, k] PW[b, r],
+// PW = p Wl (one product for every k). Block (b, k), thread r.
+__global__ void sens_dh_logit(const float* LP, const float* IG, const float* Sg, const float* PW, const float* Wl,
+                              float* dH, int Bs, int V, int K, int R, int split) {
+    const int b = blockIdx.x, k = blockIdx.y, r = threadIdx.x;
+    if (r >= R) return;
+    const float* lp = LP + (int64_t)b * V;
+    const int v0 = k * split, v1 = min(v0 + split, V);
+    float own = 0.f;
+    for (int v = v0; v < v1; ++v) own += lp[v] * Wl[(int64_t)v * R + r];
+    dH[((int64_t)k * Bs + b) * R + r] = own * IG[b * K + k] - Sg[b * K + k] * PW[(int64_t)b * R + r];
 }
 
-// LSTM cell backward for the K seeds at once: dH, dC [K, Bs, R] -> dS [K, Bs, 5R], dC <- d c_prev.
-// torch.max(a, b) (nets.py:121) splits the gradient of an exact tie in halves (aten maximum backward).
+// LSTM cell backward for the K seeds at once: dH, dC [K, Bs, R] -> dS of cell i (dS_all [K][L + 1][Bs][5R]),
+// dC <- d c_prev. torch.max(a, b) (nets.py:121) splits the gradient of an exact tie in halves (aten maximum
+// backward).
 __global__ void sens_cell_bwd(const float* dH, float* dC, const float* S, const float* C, const float* Cprev,
-                              float* dS, int K, int Bs, int R) {
+                              float* dS, int64_t sdk, int K, int Bs, int R) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)K * Bs * R) return;
     const int64_t kb = i / R;                                    // k * Bs + b
     const int r = (int)(i % R);
-    const int64_t b = kb % Bs;
+    const int64_t b = kb % Bs, k = kb / Bs;
     const float* s = S + b * 5 * R;
     const float ig = sigm(s[r]), fg = sigm(s[R + r]), og = sigm(s[2 * R + r]);
     const float g1 = s[3 * R + r], g2 = s[4 * R + r], g = fmaxf(g1, g2);
@@ -148,7 +299,7 @@ __global__ void sens_cell_bwd(const float* dH, float* dC, const float* S, const 
     const float dh = dH[i];
     const float dc = dC[i] + dh * og * (1.f - th * th);
     const float dog = dh * th;
-    float* d = dS + kb * 5 * R;
+    float* d = dS + k * sdk + b * 5 * R;
     d[r] = dc * g * ig * (1.f - ig);
     d[R + r] = dc * cp * fg * (1.f - fg);
     d[2 * R + r] = dog * og * (1.f - og);
@@ -158,27 +309,74 @@ __global__ void sens_cell_bwd(const float* dH, float* dC, const float* S, const 
     dC[i] = dc * fg;
 }
 
-// embedding rows: G[k, off + token(b) * E + e] += dX[k, b, e] (token = tok[b * stride + col], col < 0: BOS)
-__global__ void sens_embed_scatter(const float* dX, const int32_t* tok, int stride, int col, float* G, int64_t D,
-                                   int64_t off, int K, int Bs, int E) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)K * Bs * E) return;
-    const int e = (int)(i % E);
-    const int64_t kb = i / E;
-    const int b = (int)(kb % Bs), k = (int)(kb / Bs);
-    const int t = col < 0 ? 0 : tok[(int64_t)b * stride + col];
-    atomicAdd(G + (int64_t)k * D + off + (int64_t)t * E + e, dX[i]);
+// out[c] = sum_k (sum_{r < rows} X[k sk + r sr + c])^2 (a bias gradient's square sum over the K seeds);
+// out2 (nullable) gets the same
+__global__ void sens_colsum_sq(const float* X, int rows, int cols, int64_t sr, int64_t sk, int K, float* out,
+                               float* out2) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= cols) return;
+    float sq = 0.f;
+    for (int k = 0; k < K; ++k) {
+        const float* x = X + (int64_t)k * sk + c;
+        float s = 0.f;
+        for (int r = 0; r < rows; ++r) s += x[(int64_t)r * sr];
+        sq += s * s;
+    }
+    out[c] = sq;
+    if (out2) out2[c] = sq;
 }
 
-// s_j = sqrt(sum_k G[k, j]^2) / Bs, then s < underflow -> underflow, s /= underflow (safe_mutations.py:63-65)
-__global__ void sens_reduce(const float* G, int K, int64_t D, float inv_bs, float underflow, float* out) {
+// logit.bias: out[v] = sum_k (sum_b dZ[k, b, v])^2
+__global__ void sens_logb_sq(DzA A, int Bs, float* out) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= A.V) return;
+    float sq = 0.f;
+    for (int k = 0; k < A.K; ++k) {
+        float s = 0.f;
+        for (int b = 0; b < Bs; ++b) s += A(k, v, b);
+        sq += s * s;
+    }
+    out[v] = sq;
+}
+
+// embedding rows: row t gathers dX of every (cell i >= 1, row b) fed token t (BOS at cell 1, else the greedy
+// token of logit step i - 1), out[t E + e] = sum_k (sum over those (i, b) in order of dX[k, i, b, e])^2.
+// Block p = (i - 1) Bs + b handles the token of pair p if p is its first pair; thread e. dX_all [K][L + 1][Bs][E].
+__global__ void sens_emb_sq(const float* dX, const int32_t* tok, int stride, int L, int Bs, int E, int K, float* out) {
+    const int p = blockIdx.x, e = threadIdx.x;
+    const int npair = L * Bs;
+    auto token = [&](int q) {
+        const int i = q / Bs + 1, b = q % Bs;
+        return i == 1 ? 0 : tok[(int64_t)b * stride + (i - 2)];
+    };
+    const int t = token(p);
+    for (int q = 0; q < p; ++q)
+        if (token(q) == t) return;                            // not the first pair of this token
+    if (e >= E) return;
+    const int64_t sk = (int64_t)(L + 1) * Bs * E;
+    float sq = 0.f;
+    for (int k = 0; k < K; ++k) {
+        float s = 0.f;
+        for (int q = p; q < npair; ++q)
+            if (token(q) == t) s += dX[(int64_t)k * sk + ((int64_t)(q / Bs + 1) * Bs + q % Bs) * E + e];
+        sq += s * s;
+    }
+    out[(int64_t)t * E + e] = sq;
+}
+
+// s_j = sqrt(sum over the segment's range partials of part[z][j]) / Bs, then s < underflow -> underflow,
+// s /= underflow (safe_mutations.py:63-65). Segment q = [off[q], off[q + 1]) has nz[q] partial rows.
+struct Segs {
+    int64_t off[10];
+    int nz[9];
+};
+__global__ void sens_finish(const float* part, int64_t D, Segs sg, float inv_bs, float underflow, float* out) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= D) return;
+    int q = 0;
+    while (q < 8 && j >= sg.off[q + 1]) ++q;
     float acc = 0.f;
-    for (int k = 0; k < K; ++k) {
-        const float g = G[(int64_t)k * D + j];
-        acc += g * g;
-    }
+    for (int z = 0; z < sg.nz[q]; ++z) acc += part[(int64_t)z * D + j];
     float s = sqrtf(acc) * inv_bs;
     if (underflow > 0.f) {
         s = s < underflow ? underflow : s;
@@ -191,43 +389,49 @@ inline unsigned blocks(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
 }  // namespace
 
+#define SENS_NZ 16           // k-range partial rows of the square sums
+
 struct SensWork {
-    rocblas_handle blas = nullptr;
-    int Bs = 0, K = 0;
+    int Bs = 0, K = 0, L = 0;
     int64_t D = 0;
     float* X = nullptr;     // [L + 1][Bs, E] cell inputs
     float* S = nullptr;     // [L + 1][Bs, 5R] gate sums
     float* C = nullptr;     // [L + 1][Bs, R]
     float* H = nullptr;     // [L + 1][Bs, R]
-    float* Z = nullptr;     // [Bs, V] logits -> log-probs in LP
-    float* LP = nullptr;
-    float* dZ = nullptr;    // [K, Bs, V]
-    float* G = nullptr;     // [K, D] per-seed gradients, flat theta order
+    float* Z = nullptr;     // [Bs, V] logits
+    float* LP = nullptr;    // [Bs, V] log-probs
+    float* P = nullptr;     // [Bs, V] exp(log-probs)
+    float* IG = nullptr;    // [Bs, K]
+    float* SG = nullptr;    // [Bs, K]
+    float* PW = nullptr;    // [Bs, R] p Wl
     float* dH = nullptr;    // [K, Bs, R]
     float* dC = nullptr;    // [K, Bs, R]
-    float* dS = nullptr;    // [K, Bs, 5R]
-    float* dX = nullptr;    // [K, Bs, E]
+    float* dS = nullptr;    // [K][L + 1][Bs][5R]
+    float* dX = nullptr;    // [K][L + 1][Bs][E]
+    float* part = nullptr;  // [SENS_NZ][D] square-sum partials
 };
 
 namespace {
 
 void free_all(SensWork* w) {
-    float* ps[] = {w->X, w->S, w->C, w->H, w->Z, w->LP, w->dZ, w->G, w->dH, w->dC, w->dS, w->dX};
+    float* ps[] = {w->X, w->S, w->C, w->H, w->Z, w->LP, w->P, w->IG, w->SG, w->PW, w->dH, w->dC, w->dS, w->dX, w->part};
     for (float* p : ps)
         if (p) (void)hipFree(p);
-    w->X = w->S = w->C = w->H = w->Z = w->LP = w->dZ = w->G = w->dH = w->dC = w->dS = w->dX = nullptr;
-    w->Bs = w->K = 0;
+    w->X = w->S = w->C = w->H = w->Z = w->LP = w->P = w->IG = w->SG = w->PW = nullptr;
+    w->dH = w->dC = w->dS = w->dX = w->part = nullptr;
+    w->Bs = w->K = w->L = 0;
     w->D = 0;
 }
 
 hipError_t grow(SensWork* w, const SensParams* p) {
-    if (w->Bs >= p->Bs && w->K >= p->K && w->D == p->D) return hipSuccess;
+    if (w->Bs >= p->Bs && w->K >= p->K && w->L >= p->L && w->D == p->D) return hipSuccess;
     free_all(w);
     const int64_t L1 = p->L + 1, Bs = p->Bs, K = p->K, E = p->E, R = p->R, V = p->V1;
     const struct { float** q; int64_t n; } a[] = {
         {&w->X, L1 * Bs * E}, {&w->S, L1 * Bs * 5 * R}, {&w->C, L1 * Bs * R}, {&w->H, L1 * Bs * R},
-        {&w->Z, Bs * V}, {&w->LP, Bs * V}, {&w->dZ, K * Bs * V}, {&w->G, K * p->D},
-        {&w->dH, K * Bs * R}, {&w->dC, K * Bs * R}, {&w->dS, K * Bs * 5 * R}, {&w->dX, K * Bs * E}};
+        {&w->Z, Bs * V}, {&w->LP, Bs * V}, {&w->P, Bs * V}, {&w->IG, Bs * K}, {&w->SG, Bs * K}, {&w->PW, Bs * R},
+        {&w->dH, K * Bs * R}, {&w->dC, K * Bs * R}, {&w->dS, K * L1 * Bs * 5 * R}, {&w->dX, K * L1 * Bs * E},
+        {&w->part, SENS_NZ * p->D}};
     for (const auto& x : a) {
         hipError_t e = hipMalloc((void**)x.q, (size_t)x.n * sizeof(float));
         if (e != hipSuccess) {
@@ -237,19 +441,42 @@ hipError_t grow(SensWork* w, const SensParams* p) {
     }
     w->Bs = p->Bs;
     w->K = p->K;
+    w->L = p->L;
     w->D = p->D;
     return hipSuccess;
 }
 
-// row-major C[b] (M x N, ldc) = op(A[b]) (M x K) . op(B[b]) (K x N) + beta C[b], via the column-major
-// product C^T = op(B)^T op(A)^T
-rocblas_status gemm_rm(rocblas_handle hb, bool tA, bool tB, int M, int N, int Kd, const float* A, int lda,
-                       int64_t sA, const float* B, int ldb, int64_t sB, float beta, float* C, int ldc, int64_t sC,
-                       int batch) {
-    const float one = 1.f;
-    return rocblas_sgemm_strided_batched(hb, tB ? rocblas_operation_transpose : rocblas_operation_none,
-                                         tA ? rocblas_operation_transpose : rocblas_operation_none, N, M, Kd, &one, B,
-                                         ldb, sB, A, lda, sA, &beta, C, ldc, sC, batch);
+TileArgs targs(int M, int N, int R, const float* B, int64_t sBk, int64_t sBr, int64_t sBn, float* C, int64_t sCk,
+               int64_t sCm, int64_t sCn, int beta = 0) {
+    TileArgs t;
+    t.M = M; t.N = N; t.R = R;
+    t.B = B; t.sBk = sBk; t.sBr = sBr; t.sBn = sBn;
+    t.C = C; t.sCk = sCk; t.sCm = sCm; t.sCn = sCn;
+    t.beta = beta;
+    t.k0 = 0; t.kpr = 1; t.k_end = 1;
+    return t;
+}
+
+// C_k = A_k B_k for k < batch
+template <class AOp>
+void gemm(const AOp& A, const TileArgs& t, int batch, hipStream_t st) {
+    hipLaunchKernelGGL((sens_tile<AOp, false>), dim3(blocks(t.M, TM), blocks(t.N, TN), batch), dim3(256), 0, st, A, t);
+}
+
+// part[z][out + m sCm + n] = sum over the k of range z of (A_k B)[m, n]^2, nz ranges over k < K
+template <class AOp>
+void sqsum(const AOp& A, TileArgs t, int K, int nz, hipStream_t st) {
+    t.k0 = 0;
+    t.kpr = (K + nz - 1) / nz;
+    t.k_end = K;
+    const int z = (K + t.kpr - 1) / t.kpr;
+    hipLaunchKernelGGL((sens_tile<AOp, true>), dim3(blocks(t.M, TM), blocks(t.N, TN), z), dim3(256), 0, st, A, t);
+}
+
+Strided sa(const float* p, int64_t sk, int64_t sm, int64_t sr) {
+    Strided s;
+    s.p = p; s.sk = sk; s.sm = sm; s.sr = sr;
+    return s;
 }
 
 }  // namespace
@@ -259,85 +486,93 @@ extern "C" SensWork* nicnes_sens_create() { return new SensWork(); }
 extern "C" void nicnes_sens_destroy(SensWork* w) {
     if (!w) return;
     free_all(w);
-    if (w->blas) (void)rocblas_destroy_handle(w->blas);
     delete w;
 }
 
 extern "C" int nicnes_sens_run(SensWork* w, const SensParams* p, hipStream_t st) {
     if (!w || !p || p->Bs < 1 || p->L < 1 || p->split < 1) return 1;
-    if (!w->blas) {
-        if (rocblas_create_handle(&w->blas) != rocblas_status_success) return 2;
-    }
-    if (rocblas_set_stream(w->blas, st) != rocblas_status_success) return 2;
+    if (p->E > 256 || p->R > 256) return 1;                     // thread-per-column kernels
     if (grow(w, p) != hipSuccess) return 3;
-    const int Bs = p->Bs, E = p->E, R = p->R, F = p->F, V = p->V1, K = p->K, L = p->L;
-    const int64_t D = p->D;
+    const int Bs = p->Bs, E = p->E, R = p->R, F = p->F, V = p->V1, K = p->K, L = p->L, G5 = 5 * R;
+    const int64_t D = p->D, L1 = L + 1;
     const float* th = p->theta;
     const float *Wimg = th + p->off_img_w, *bimg = th + p->off_img_b, *Wemb = th + p->off_emb_w;
     const float *Wl = th + p->off_log_w, *bl = th + p->off_log_b;
     const float *Wi = th + p->off_i2h_w, *bi = th + p->off_i2h_b, *Wh = th + p->off_h2h_w, *bh = th + p->off_h2h_b;
     auto Xs = [&](int i) { return w->X + (int64_t)i * Bs * E; };
-    auto Ss = [&](int i) { return w->S + (int64_t)i * Bs * 5 * R; };
+    auto Ss = [&](int i) { return w->S + (int64_t)i * Bs * G5; };
     auto Cs = [&](int i) { return w->C + (int64_t)i * Bs * R; };
     auto Hs = [&](int i) { return w->H + (int64_t)i * Bs * R; };
     // token fed to cell i (1..L): BOS for i = 1, else the greedy token of logit step i - 1
     auto tok_col = [&](int i) { return i == 1 ? -1 : i - 2; };
-    rocblas_status bs = rocblas_status_success;
-    auto G = [&](rocblas_status s) { if (s != rocblas_status_success) bs = s; };
 
-    // ---- forward: image cell, then L token cells (forward_for_sensitivity, nets.py:48-64)
-    G(gemm_rm(w->blas, false, true, Bs, E, F, p->fc, F, 0, Wimg, F, 0, 0.f, Xs(0), E, 0, 1));   // img_embed
+    // ---- forward: image cell, then L token cells (forward_for_sensitivity, nets.py:48-64); C = A B with
+    // A row-major [rows, red] and B = W^T of a row-major [out, in] weight
+    gemm(sa(p->fc, 0, F, 1), targs(Bs, E, F, Wimg, 0, 1, F, Xs(0), 0, E, 1), 1, st);          // img_embed
     hipLaunchKernelGGL(sens_bias_rows, dim3(blocks((int64_t)Bs * E, 256)), dim3(256), 0, st, Xs(0), bimg,
                        (const float*)nullptr, Bs, E);
     for (int i = 0; i <= L; ++i) {
         if (i >= 1)
             hipLaunchKernelGGL(sens_embed_gather, dim3(Bs), dim3(E), 0, st, Xs(i), Wemb, p->tok, p->tok_stride,
                                tok_col(i), Bs, E);
-        G(gemm_rm(w->blas, false, true, Bs, 5 * R, E, Xs(i), E, 0, Wi, E, 0, 0.f, Ss(i), 5 * R, 0, 1));
-        if (i >= 1) G(gemm_rm(w->blas, false, true, Bs, 5 * R, R, Hs(i - 1), R, 0, Wh, R, 0, 1.f, Ss(i), 5 * R, 0, 1));
-        hipLaunchKernelGGL(sens_bias_rows, dim3(blocks((int64_t)Bs * 5 * R, 256)), dim3(256), 0, st, Ss(i), bi, bh,
-                           Bs, 5 * R);
+        gemm(sa(Xs(i), 0, E, 1), targs(Bs, G5, E, Wi, 0, 1, E, Ss(i), 0, G5, 1), 1, st);          // i2h
+        if (i >= 1) gemm(sa(Hs(i - 1), 0, R, 1), targs(Bs, G5, R, Wh, 0, 1, R, Ss(i), 0, G5, 1, 1), 1, st);   // h2h
+        hipLaunchKernelGGL(sens_bias_rows, dim3(blocks((int64_t)Bs * G5, 256)), dim3(256), 0, st, Ss(i), bi, bh, Bs, G5);
         hipLaunchKernelGGL(sens_cell_fwd, dim3(blocks((int64_t)Bs * R, 256)), dim3(256), 0, st, Ss(i),
                            i ? (const float*)Cs(i - 1) : (const float*)nullptr, Cs(i), Hs(i), Bs, R);
     }
-    G(gemm_rm(w->blas, false, true, Bs, V, R, Hs(L), R, 0, Wl, R, 0, 0.f, w->Z, V, 0, 1));        // logit
+    gemm(sa(Hs(L), 0, R, 1), targs(Bs, V, R, Wl, 0, 1, R, w->Z, 0, V, 1), 1, st);               // logit
     hipLaunchKernelGGL(sens_bias_rows, dim3(blocks((int64_t)Bs * V, 256)), dim3(256), 0, st, w->Z, bl,
                        (const float*)nullptr, Bs, V);
-    hipLaunchKernelGGL(sens_logsoftmax, dim3(Bs), dim3(256), 0, st, w->Z, w->LP, V);
+    hipLaunchKernelGGL(sens_logsoftmax, dim3(Bs), dim3(256), 0, st, w->Z, w->LP, w->P, V);
 
     // ---- the K backward passes at once
-    hipLaunchKernelGGL(sens_seed, dim3(Bs, K), dim3(128), 0, st, w->LP, w->dZ, Bs, V, p->split);
-    if (hipMemsetAsync(w->G, 0, (size_t)K * D * sizeof(float), st) != hipSuccess) return 4;
-    const int64_t sZ = (int64_t)Bs * V;
-    // logit.weight / .bias, dh of the last cell
-    G(gemm_rm(w->blas, true, false, V, R, Bs, w->dZ, V, sZ, Hs(L), R, 0, 0.f, w->G + p->off_log_w, R, D, K));
-    hipLaunchKernelGGL(sens_colsum, dim3(blocks(V, 256), K), dim3(256), 0, st, w->dZ, Bs, V, sZ, w->G + p->off_log_b,
-                       (float*)nullptr, D, 0);
-    G(gemm_rm(w->blas, false, false, Bs, R, V, w->dZ, V, sZ, Wl, R, 0, 0.f, w->dH, R, (int64_t)Bs * R, K));
+    hipLaunchKernelGGL(sens_seed, dim3(Bs, K), dim3(128), 0, st, w->LP, w->IG, w->SG, Bs, V, K, p->split);
+    DzA dz;
+    dz.lp = w->LP; dz.pr = w->P; dz.ig = w->IG; dz.S = w->SG; dz.V = V; dz.K = K; dz.split = p->split;
+    float* part = w->part;
+    // logit.weight: G_k[v, r] = sum_b dZ_k[b, v] H_L[b, r]; logit.bias
+    sqsum(dz, targs(V, R, Bs, Hs(L), 0, R, 1, part + p->off_log_w, D, R, 1), K, SENS_NZ, st);
+    hipLaunchKernelGGL(sens_logb_sq, dim3(blocks(V, 256)), dim3(256), 0, st, dz, Bs, part + p->off_log_b);
+    // dH of the last cell: p Wl once, then the group terms
+    gemm(sa(w->P, 0, V, 1), targs(Bs, R, V, Wl, 0, R, 1, w->PW, 0, R, 1), 1, st);
+    hipLaunchKernelGGL(sens_dh_logit, dim3(Bs, K), dim3(R), 0, st, w->LP, w->IG, w->SG, w->PW, Wl, w->dH, Bs, V, K, R,
+                       p->split);
     if (hipMemsetAsync(w->dC, 0, (size_t)K * Bs * R * sizeof(float), st) != hipSuccess) return 4;
-    const int64_t sS = (int64_t)Bs * 5 * R, sX = (int64_t)Bs * E, sH = (int64_t)Bs * R;
+    const int64_t sdk = L1 * Bs * G5, sxk = L1 * Bs * E;
     for (int i = L; i >= 0; --i) {
+        float* dSi = w->dS + (int64_t)i * Bs * G5;
         hipLaunchKernelGGL(sens_cell_bwd, dim3(blocks((int64_t)K * Bs * R, 256)), dim3(256), 0, st, w->dH, w->dC, Ss(i),
-                           Cs(i), i ? (const float*)Cs(i - 1) : (const float*)nullptr, w->dS, K, Bs, R);
-        G(gemm_rm(w->blas, true, false, 5 * R, E, Bs, w->dS, 5 * R, sS, Xs(i), E, 0, 1.f, w->G + p->off_i2h_w, E, D, K));
+                           Cs(i), i ? (const float*)Cs(i - 1) : (const float*)nullptr, dSi, sdk, K, Bs, R);
+        // dX_i = dS_i Wi ([5R, E] row-major), dH_{i-1} = dS_i Wh
+        gemm(sa(dSi, sdk, G5, 1), targs(Bs, E, G5, Wi, 0, E, 1, w->dX + (int64_t)i * Bs * E, sxk, E, 1), K, st);
         if (i >= 1)
-            G(gemm_rm(w->blas, true, false, 5 * R, R, Bs, w->dS, 5 * R, sS, Hs(i - 1), R, 0, 1.f, w->G + p->off_h2h_w,
-                      R, D, K));
-        hipLaunchKernelGGL(sens_colsum, dim3(blocks(5 * R, 256), K), dim3(256), 0, st, w->dS, Bs, 5 * R, sS,
-                           w->G + p->off_i2h_b, w->G + p->off_h2h_b, D, 1);
-        G(gemm_rm(w->blas, false, false, Bs, E, 5 * R, w->dS, 5 * R, sS, Wi, E, 0, 0.f, w->dX, E, sX, K));
-        if (i >= 1) {
-            G(gemm_rm(w->blas, false, false, Bs, R, 5 * R, w->dS, 5 * R, sS, Wh, R, 0, 0.f, w->dH, R, sH, K));
-            hipLaunchKernelGGL(sens_embed_scatter, dim3(blocks((int64_t)K * Bs * E, 256)), dim3(256), 0, st, w->dX,
-                               p->tok, p->tok_stride, tok_col(i), w->G, D, p->off_emb_w, K, Bs, E);
-        } else {
-            G(gemm_rm(w->blas, true, false, E, F, Bs, w->dX, E, sX, p->fc, F, 0, 0.f, w->G + p->off_img_w, F, D, K));
-            hipLaunchKernelGGL(sens_colsum, dim3(blocks(E, 256), K), dim3(256), 0, st, w->dX, Bs, E, sX,
-                               w->G + p->off_img_b, (float*)nullptr, D, 0);
-        }
+            gemm(sa(dSi, sdk, G5, 1), targs(Bs, R, G5, Wh, 0, R, 1, w->dH, (int64_t)Bs * R, R, 1), K, st);
     }
-    hipLaunchKernelGGL(sens_reduce, dim3(blocks(D, 256)), dim3(256), 0, st, w->G, K, D, 1.f / (float)Bs, p->underflow,
+    // gate weights: G_k[g, e] = sum over (cell i, b) of dS_k[i, b, g] X_i[b, e] (h2h: cells 1..L with H_{i-1})
+    sqsum(sa(w->dS, sdk, 1, G5), targs(G5, E, (int)(L1 * Bs), w->X, 0, E, 1, part + p->off_i2h_w, D, E, 1), K, SENS_NZ, st);
+    sqsum(sa(w->dS + (int64_t)Bs * G5, sdk, 1, G5), targs(G5, R, L * Bs, w->H, 0, R, 1, part + p->off_h2h_w, D, R, 1), K,
+          SENS_NZ, st);
+    // both gate biases take every cell's dS (h2h's bias is added at cell 0 too, where h = 0)
+    hipLaunchKernelGGL(sens_colsum_sq, dim3(blocks(G5, 256)), dim3(256), 0, st, w->dS, (int)(L1 * Bs), G5, (int64_t)G5,
+                       sdk, K, part + p->off_i2h_b, part + p->off_h2h_b);
+    // img_embed: G_k[e, f] = sum_b dX_k[0, b, e] fc[b, f]; its bias
+    sqsum(sa(w->dX, sxk, 1, E), targs(E, F, Bs, p->fc, 0, F, 1, part + p->off_img_w, D, F, 1), K, SENS_NZ, st);
+    hipLaunchKernelGGL(sens_colsum_sq, dim3(blocks(E, 256)), dim3(256), 0, st, w->dX, Bs, E, (int64_t)E, sxk, K,
+                       part + p->off_img_b, (float*)nullptr);
+    // embedding rows never fed stay 0
+    if (hipMemsetAsync(part + p->off_emb_w, 0, (size_t)(p->off_log_w - p->off_emb_w) * sizeof(float), st) != hipSuccess)
+        return 4;
+    hipLaunchKernelGGL(sens_emb_sq, dim3(L * Bs), dim3(E), 0, st, w->dX, p->tok, p->tok_stride, L, Bs, E, K,
+                       part + p->off_emb_w);
+    Segs sg;
+    const int64_t offs[10] = {p->off_img_w, p->off_img_b, p->off_emb_w, p->off_log_w, p->off_log_b,
+                              p->off_i2h_w, p->off_i2h_b, p->off_h2h_w, p->off_h2h_b, D};
+    const int kpr = (K + SENS_NZ - 1) / SENS_NZ, nzk = (K + kpr - 1) / kpr;
+    const int nz[9] = {nzk, 1, 1, nzk, 1, nzk, 1, nzk, 1};     // weights: k-range partials; the rest: one row
+    for (int q = 0; q < 10; ++q) sg.off[q] = offs[q];
+    for (int q = 0; q < 9; ++q) sg.nz[q] = nz[q];
+    hipLaunchKernelGGL(sens_finish, dim3(blocks(D, 256)), dim3(256), 0, st, part, D, sg, 1.f / (float)Bs, p->underflow,
                        p->out);
-    if (bs != rocblas_status_success) return 5;
     return hipGetLastError() == hipSuccess ? 0 : 6;
 }

@@ -1,6 +1,6 @@
 """TEST INFRASTRUCTURE (oracle): the SM-G-SUM sensitivity restated with torch autograd on the CPU.
 
-Follows Sensitivity._calc_sum_sensitivity (/root/reference/src/algorithm/safe_mutations.py:86-110) on
+Follows Sensitivity._calc_sum_sensitivity (/root/reference/src/algorithm/safe_mutations.py:93-117) on
 CaptionModel.forward_for_sensitivity (/root/reference/src/captioning/nets.py:22-70) and LSTMCore
 (nets.py:75-134) in the reference's op order; tests/golden/mutations.npz pins it bit for bit against the
 reference's own calc_sensitivity. The engine computes the same vector on the GPU
@@ -70,7 +70,7 @@ class SensitivityNet(nn.Module):
 
 
 def sum_sensitivity(dims, theta32, fc_unique, orig_bs):
-    """Sensitivity._calc_sum_sensitivity (safe_mutations.py:86-110): per parameter, the 2-norm over
+    """Sensitivity._calc_sum_sensitivity (safe_mutations.py:93-117): per parameter, the 2-norm over
     the grouped outputs of d(output summed over the batch)/d(theta), divided by the batch size.
     dims = (V1, E, R, F). Returns fp32 [D] (before the underflow clamp)."""
     net = SensitivityNet(*dims)

@@ -94,11 +94,12 @@ def _sens_close(gpu, ref):
     return bool((err <= bound).all()), float((err / np.maximum(np.abs(ref), 1e-30))[np.abs(ref) > 1e-3 * np.abs(ref).max()].max())
 
 
-@pytest.mark.parametrize('theta_kind,rows', [('xavier', 8), ('wc', 16)])
+@pytest.mark.parametrize('theta_kind,rows', [('xavier', 8), ('wc', 16), ('wc', 41)])
 def test_gpu_sensitivity_matches_oracle(theta_kind, rows):
-    """nicnes_sum_sensitivity (95 backward passes batched on the GPU) against the torch-autograd restatement
-    oracle/sensitivity_ref.py, itself bit-exact with the reference's Sensitivity.calc_sensitivity
-    (tests/golden/mutations.npz): the raw vector and the clamped one (underflow 0.1, mscoco_nes.json)."""
+    """nicnes_sum_sensitivity (95 backward passes batched on the GPU, the square sums fused into the MFMA tile
+    kernels) against the torch-autograd restatement oracle/sensitivity_ref.py, itself bit-exact with the
+    reference's Sensitivity.calc_sensitivity (tests/golden/mutations.npz): the raw vector and the clamped one
+    (underflow 0.1, mscoco_nes.json). Bit-identical from call to call (no atomics: ADVICE r03)."""
     import nicnes
     from nicnes import mutations as MU
     from oracle import sensitivity_ref as SR
@@ -113,6 +114,7 @@ def test_gpu_sensitivity_matches_oracle(theta_kind, rows):
         e.set_batch(fc, [np.zeros((1, dims.T), np.int32)] * fc.shape[0])
         raw = e.sum_sensitivity(rows).cpu().numpy()
         clamped = e.sum_sensitivity(rows, 0.1).cpu().numpy()
+        assert np.array_equal(e.sum_sensitivity(rows).cpu().numpy(), raw)
     finally:
         e.close()
     ref = SR.sum_sensitivity((dims.vocab_size + 1, dims.E, dims.R, dims.F), theta, fc[:rows], rows).numpy()
