@@ -330,16 +330,18 @@ __global__ __launch_bounds__(64) void nicnes_img_ngram_kernel(const int32_t* img
 // Grid (candidate, row block of CIDER_IMG_ROWS): the probe chains are latency-bound, so each
 // candidate's rows are spread over several workgroups; per-row scores go to `scores` [n_cand, B]
 // and nicnes_cider_finish_kernel reduces them in row order, as the single-workgroup form did.
+// Rows per workgroup: 32, or 8 when there are few candidates (64 members per GPU: 128 candidates), so that the
+// launch still has >= ~2048 workgroups to hide the probe latency (the P = 64 rollouts: DESIGN §5).
 #define CIDER_IMG_ROWS 32
 __global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* seq, int B, int T, CiderTables tb,
                                                                const int32_t* img_ref_start, const int32_t* member_batch,
-                                                               double* scores, int rpi) {
+                                                               double* scores, int rpi, int rows_wg) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int cand = blockIdx.x;
     const int img0 = member_batch ? member_batch[cand >> 1] * (B / rpi) : 0;   // this member's batch (single_batch: false)
-    const int b_end = min(B, (int)(blockIdx.y + 1) * CIDER_IMG_ROWS);
+    const int b_end = min(B, (int)(blockIdx.y + 1) * rows_wg);
     const double sigma2x2 = 2.0 * 6.0 * 6.0;
-    for (int b = (int)blockIdx.y * CIDER_IMG_ROWS + wave; b < b_end; b += 4) {
+    for (int b = (int)blockIdx.y * rows_wg + wave; b < b_end; b += 4) {
         const int32_t* row = seq + ((size_t)cand * B + b) * T;
         const NgramLane g = ngram_lane(row, T, lane, tb);
         const double nh = sqrt(seg_sum(g.first ? g.vec * g.vec : 0.0));
@@ -400,8 +402,9 @@ extern "C" hipError_t nicnes_launch_cider_img(const int32_t* seq, int n_cand, in
                                               int crit, double* scores, double* fitness_out, hipStream_t stream,
                                               const double* base, int rpi) {
     if (B > 1024 || n_cand < 1 || rpi < 1 || B % rpi) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(nicnes_cider_img_kernel, dim3(n_cand, (B + CIDER_IMG_ROWS - 1) / CIDER_IMG_ROWS), dim3(256), 0,
-                       stream, seq, B, T, *tb, img_ref_start, member_batch, scores, rpi);
+    const int rows_wg = (int64_t)n_cand * ((B + CIDER_IMG_ROWS - 1) / CIDER_IMG_ROWS) >= 2048 ? CIDER_IMG_ROWS : 8;
+    hipLaunchKernelGGL(nicnes_cider_img_kernel, dim3(n_cand, (B + rows_wg - 1) / rows_wg), dim3(256), 0,
+                       stream, seq, B, T, *tb, img_ref_start, member_batch, scores, rpi, rows_wg);
     hipLaunchKernelGGL(nicnes_cider_finish_kernel, dim3(n_cand), dim3(256), 0, stream, seq, B, T, (const double*)scores,
                        lp, crit, fitness_out, base, rpi, tb->fault);
     return hipGetLastError();

@@ -751,6 +751,11 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
 // b (16 each), word 8 = {P (fp64), r, 0}.
 #define SLOG_WAVE_BYTES 9216u                  // 9 words x 64 lanes x 16 bytes
 #define SLOG_STAGE_BYTES (8u * SLOG_WAVE_BYTES)  // one 64-row stage of a workgroup (72 KiB)
+// after the nst stages: one record per block of SLOG_BLOCK stages, {B (fp64), r, 0} per lane (8 waves x 1 KiB):
+// the lane's sum of the block's terms relative to 2^r, so the pick finds the crossing block in two rounds of
+// loads and then the crossing stage in one
+#define SLOG_BLOCK 8
+#define SLOG_BLK_BYTES 8192u
 #define SLOT_SPIN_TICKS 50000000ull   // 0.5 s of s_memrealtime (100 MHz) to find a free logit slot
 #ifndef SLOG_STORE_POLICY
 #define SLOG_STORE_POLICY 0      // cache policy of the slot stores (2: nt, streaming past the L2's normal allocation)
@@ -785,9 +790,12 @@ struct SampleStage {
     static constexpr bool replaces = true;
     rsrc_t slot;
     uint32_t vo;      // 16 * lane + SLOG_WAVE_BYTES * wave
+    uint32_t vb;      // 16 * lane + 1024 * wave (block records)
+    int nst;          // stages per step
     float& m;
     float& ref;
     double& T;
+    double& Bk;       // the current block's sum of terms relative to 2^ref
     __device__ __forceinline__ void operator()(const f32x16& q0, const f32x16& q1, int s) const {
         if (s < 0) return;                               // the pipeline's first epilogue: no stage yet
         const uint32_t so = SLOG_STAGE_BYTES * (uint32_t)s;
@@ -804,6 +812,7 @@ struct SampleStage {
         const float rnew = ceilf(mnew * LOG2E);
         if (rnew > ref) {
             T = samp_scale(T, ref - rnew);
+            Bk = samp_scale(Bk, ref - rnew);
             ref = rnew;
         }
         m = mnew;
@@ -820,9 +829,18 @@ struct SampleStage {
             P += (double)samp_group(qb);
         }
         T += P;
+        Bk += P;
         const uint64_t pb = __builtin_bit_cast(uint64_t, P);
         const u32x4 w = {(uint32_t)pb, (uint32_t)(pb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
         __builtin_amdgcn_raw_buffer_store_b128(w, slot, (int)vo, (int)(so + 8u * 1024u), SLOG_STORE_POLICY);
+        if ((s % SLOG_BLOCK) == SLOG_BLOCK - 1 || s == nst - 1) {      // the block's record (wave-uniform branch)
+            const uint64_t bb = __builtin_bit_cast(uint64_t, Bk);
+            const u32x4 wb = {(uint32_t)bb, (uint32_t)(bb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
+            __builtin_amdgcn_raw_buffer_store_b128(wb, slot, (int)vb,
+                                                   (int)(SLOG_STAGE_BYTES * (uint32_t)nst + SLOG_BLK_BYTES * (uint32_t)(s / SLOG_BLOCK)),
+                                                   SLOG_STORE_POLICY);
+            Bk = 0.0;
+        }
     }
 };
 
@@ -902,36 +920,60 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
         }
         if (found) sf = -1;
     } else {
-        bool have = false;
-        double cl = 0.0;
-        float rl = 0.f;
-        for (int s0 = 0; s0 < nst; s0 += 8) {
-            // P and r as their own loads (a 16-byte load narrowed by the compiler returned P's low word as r)
-            double Pw[8];
-            float rw[8];
+        // level 1: the block records (both lanes of a row sum the same values in the same order)
+        const int nblk = (nst + SLOG_BLOCK - 1) / SLOG_BLOCK;
+        const uint32_t vb = 16u * (uint32_t)(threadIdx.x & 63) + 1024u * (uint32_t)(threadIdx.x >> 6);
+        int qf = -1;
+        double cq = 0.0, cl = 0.0;
+        for (int q0 = 0; q0 < nblk; q0 += 10) {
+            // B and r as their own loads (a 16-byte load narrowed by the compiler returned B's low word as r)
+            double Bw[10];
+            float rw[10];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int so = (int)(SLOG_STAGE_BYTES * min(s0 + j, nst - 1) + 8u * 1024u);
-                Pw[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lr, (int)vo, so, 16));
-                rw[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (int)vo + 8, so, 16));
+            for (int j = 0; j < 10; ++j) {
+                const int so = (int)(SLOG_STAGE_BYTES * (uint32_t)nst + SLOG_BLK_BYTES * (uint32_t)min(q0 + j, nblk - 1));
+                Bw[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lr, (int)vb, so, 16));
+                rw[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (int)vb + 8, so, 16));
             }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if (s0 + j < nst) {
-                    const double P = Pw[j];
-                    const float r = rw[j];
-                    const double a = samp_scale(P, r - R);
+            for (int j = 0; j < 10; ++j) {
+                if (q0 + j < nblk) {
+                    const double a = samp_scale(Bw[j], rw[j] - R);
                     const double ao = __shfl_xor(a, 32);
                     const double S = hh == 0 ? a + ao : ao + a;
-                    if (!have) {
-                        if (cum + S > thr) { have = true; sf = s0 + j; cb = cum; rf = r; }
-                        else { cl = cum; rl = r; cum += S; }
+                    if (qf < 0) {
+                        if (cum + S > thr) { qf = q0 + j; cq = cum; }
+                        else { cl = cum; cum += S; }
                     }
                 }
             }
-            if (__all(have ? 1 : 0)) break;
+            if (__all(qf >= 0 ? 1 : 0)) break;
         }
-        if (!have) { sf = nst - 1; cb = cl; rf = rl; }
+        if (qf < 0) { qf = nblk - 1; cq = cl; }                 // thr at the very end (rounding): the last block
+        // level 2: the stage records of block qf (a per-lane block: the stage offset goes in the vector offset)
+        const int sa = SLOG_BLOCK * qf, sn = min(SLOG_BLOCK, nst - sa);
+        double Pw[SLOG_BLOCK];
+        float rw[SLOG_BLOCK];
+#pragma unroll
+        for (int j = 0; j < SLOG_BLOCK; ++j) {
+            const uint32_t o = vo + SLOG_STAGE_BYTES * (uint32_t)(sa + min(j, sn - 1)) + 8u * 1024u;
+            Pw[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lr, (int)o, 0, 16));
+            rw[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (int)o + 8, 0, 16));
+        }
+        bool have = false;
+        double cs = cq, csl = cq;
+        float rl = rw[0];
+#pragma unroll
+        for (int j = 0; j < SLOG_BLOCK; ++j) {
+            const double a = samp_scale(Pw[j], rw[j] - R);
+            const double ao = __shfl_xor(a, 32);
+            const double S = hh == 0 ? a + ao : ao + a;
+            if (!have && j < sn) {
+                if (cs + S > thr) { have = true; sf = sa + j; cb = cs; rf = rw[j]; }
+                else { csl = cs; rl = rw[j]; cs += S; }
+            }
+        }
+        if (!have) { sf = sa + sn - 1; cb = csl; rf = rl; }     // the block's stage sums stop short: its last stage
         f32x16 x0, x1;
         samp_load_stage(lr, vo, SLOG_STAGE_BYTES * (uint32_t)sf, x0, x1);
         sample_stage_walk(x0, x1, sf, hh, rf, __builtin_ldexp(1.0, (int)fmaxf(rf - R, -2000.f)), m, lse, thr, cb, found,
@@ -1383,9 +1425,11 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         };
         // SAMPLE: the lane's running max, reference and sum of terms (SampleStage), the logits to the slot
         float sm = -1.0e30f, sref = -1.0e30f;
-        double sT = 0.0;
+        double sT = 0.0, sB = 0.0;
         if constexpr (SAMPLE) {
-            const SampleStage ss{c.slog_r, 16u * (uint32_t)lane_fresh() + SLOG_WAVE_BYTES * (uint32_t)c.wave, sm, sref, sT};
+            const SampleStage ss{c.slog_r, 16u * (uint32_t)lane_fresh() + SLOG_WAVE_BYTES * (uint32_t)c.wave,
+                                 16u * (uint32_t)lane_fresh() + 1024u * (uint32_t)c.wave, (p.V1 + 63) >> 6, sm, sref, sT,
+                                 sB};
             logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail, ss);
         } else {
             logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail);
@@ -1624,7 +1668,8 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodePar
         slot = slot_sh;
         if (slot < 0) return;
         const int nst = (p.V1 + 63) >> 6;
-        c.slog_r = make_rsrc(p.slog + (size_t)slot * nst * (SLOG_STAGE_BYTES / 4), SLOG_STAGE_BYTES * (uint32_t)nst);
+        const uint32_t sbytes = SLOG_STAGE_BYTES * (uint32_t)nst + SLOG_BLK_BYTES * (uint32_t)((nst + SLOG_BLOCK - 1) / SLOG_BLOCK);
+        c.slog_r = make_rsrc(p.slog + (size_t)slot * (sbytes / 4), sbytes);
         static_assert(SLOG_STAGE_BYTES % 4 == 0, "slot stage size");
     }
     wave_prio(c.wave);

@@ -866,7 +866,9 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
             // a slot per resident workgroup (one per CU: the steps kernel's LDS) plus spares, each holding one
             // step's logits and stage sums of a workgroup's 2 x 128 rows (nst stages of 72 KiB)
             const int ns = h->test_slots > 0 ? h->test_slots : h->sample_occ * h->n_cu + 16;
-            const size_t per = (size_t)((h->V1 + 63) / 64) * 18432;   // 72 KiB per stage (decode_kernel.hip)
+            // 72 KiB per stage + 8 KiB per block of 8 stages (decode_kernel.hip, SLOG_*)
+            const int nst = (h->V1 + 63) / 64;
+            const size_t per = (size_t)nst * 18432 + (size_t)((nst + 7) / 8) * 2048;
             HIPC(h, hipDeviceSynchronize());
             int rc = dalloc(h, &h->slog, per * ns);
             if (!rc) rc = dalloc(h, &h->slog_slots, (size_t)ns);

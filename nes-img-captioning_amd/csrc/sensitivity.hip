@@ -25,14 +25,14 @@
 // another order), not bit for bit.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "sensitivity.h"
+#include "../../include/nicnes_math.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
-
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
 // ---- the tile kernel -----------------------------------------------------------------------------
 // C[m, n] = sum_r A(k, m, r) B(k, r, n) over a 64 x 64 tile per workgroup of 4 waves (wave w: rows
@@ -78,7 +78,12 @@ struct TileArgs {
     int64_t sCk, sCm, sCn;
     int beta;                // gemm: 1 accumulate into C
     int k0, kpr, k_end;      // sq: range z covers k in [k0 + z kpr, min(k0 + (z + 1) kpr, k_end))
+    const float* bias;       // gemm (nullable): every column's chain starts from bias[n] (and beta is 0)
+    int kperm;               // 1: the reduction visits r in the reference's fma-chain order (nn_kperm)
 };
+
+// nn_kperm inside a 16-aligned chunk: chain position p -> r (the 32-wide pattern keeps each half in its 16)
+__device__ __forceinline__ int perm16(int p) { const int j = p >> 1; return (j & 3) + 8 * (j >> 2) + 4 * (p & 1); }
 
 // chunk [r0, r0 + TR) of A (TM rows from m0) and B (TN columns from n0) into registers: 4 + 4 values per
 // thread, the 256 threads laid along the operand's unit-stride dimension
@@ -91,7 +96,7 @@ __device__ __forceinline__ void tile_load(const AOp& A, const TileArgs& t, int k
     for (int e = 0; e < 4; ++e) {
         const int i = tid + 256 * e;
         const int m = am ? (i & (TM - 1)) : (i >> 4), r = am ? (i >> 6) : (i & (TR - 1));
-        const int gm = m0 + m, gr = r0 + r;
+        const int gm = m0 + m, gr = r0 + (t.kperm ? perm16(r) : r);
         ra[e] = (gm < t.M && gr < t.R) ? A(k, gm, gr) : 0.f;
     }
     const bool bn = t.sBn == 1;
@@ -99,7 +104,7 @@ __device__ __forceinline__ void tile_load(const AOp& A, const TileArgs& t, int k
     for (int e = 0; e < 4; ++e) {
         const int i = tid + 256 * e;
         const int n = bn ? (i & (TN - 1)) : (i >> 4), r = bn ? (i >> 6) : (i & (TR - 1));
-        const int gn = n0 + n, gr = r0 + r;
+        const int gn = n0 + n, gr = r0 + (t.kperm ? perm16(r) : r);
         rb[e] = (gn < t.N && gr < t.R) ? t.B[(int64_t)k * t.sBk + (int64_t)gr * t.sBr + (int64_t)gn * t.sBn] : 0.f;
     }
 }
@@ -151,9 +156,11 @@ __global__ __launch_bounds__(256) void sens_tile(AOp A, TileArgs t) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) sq[i] = 0.f;
     const int ka = SQ ? t.k0 + z * t.kpr : z, kb = SQ ? min(ka + t.kpr, t.k_end) : z + 1;
+    // the bias the gemm's chains start from (the reference's addmm order: nicnes_math.h nn_kperm)
+    const float b0 = (!SQ && t.bias && n0 + wn + li < t.N) ? t.bias[n0 + wn + li] : 0.f;
     for (int k = ka; k < kb; ++k) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+        for (int i = 0; i < 16; ++i) acc[i] = b0;
         tile_product(A, t, k, m0, n0, As, Bs, acc);
         if (SQ) {
 #pragma unroll
@@ -174,14 +181,6 @@ __global__ __launch_bounds__(256) void sens_tile(AOp A, TileArgs t) {
 }
 
 // ---- elementwise and small kernels ------------------------------------------------------------------
-// Y[r, c] += b1[c] (+ b2[c])
-__global__ void sens_bias_rows(float* Y, const float* b1, const float* b2, int rows, int cols) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)rows * cols) return;
-    const int c = (int)(i % cols);
-    Y[i] += b1[c] + (b2 ? b2[c] : 0.f);
-}
-
 // X[b, :] = emb[token, :], token = tok[b * stride + col] (col < 0: the BOS token 0)
 __global__ void sens_embed_gather(float* X, const float* emb, const int32_t* tok, int stride, int col, int Bs, int E) {
     const int b = blockIdx.x, e = threadIdx.x;
@@ -190,18 +189,21 @@ __global__ void sens_embed_gather(float* X, const float* emb, const int32_t* tok
     X[(int64_t)b * E + e] = emb[(int64_t)t * E + e];
 }
 
-// LSTMCore without vbn / layer norm (nets.py:98-134): S = [Bs, 5R] gate sums (i, f, o, g1, g2)
-__global__ void sens_cell_fwd(const float* S, const float* Cprev, float* C, float* H, int Bs, int R) {
+// LSTMCore without vbn / layer norm (nets.py:98-134): S = [Bs, 5R] gate sums (i, f, o, g1, g2) = the i2h chain
+// (in S) + the h2h chain (Sh, nullable: the bias alone, h = 0), then the cell as the decode runs it (nn_lstm_cell)
+__global__ void sens_cell_fwd(float* S, const float* Sh, const float* bh, const float* Cprev, float* C, float* H, int Bs,
+                              int R) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)Bs * R) return;
     const int64_t b = i / R;
     const int r = (int)(i % R);
-    const float* s = S + b * 5 * R;
-    const float ig = sigm(s[r]), fg = sigm(s[R + r]), og = sigm(s[2 * R + r]);
-    const float g = fmaxf(s[3 * R + r], s[4 * R + r]);
-    const float c = fg * (Cprev ? Cprev[i] : 0.f) + ig * g;
-    C[i] = c;
-    H[i] = og * tanhf(c);
+    float* s = S + b * 5 * R;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) s[q * R + r] = s[q * R + r] + (Sh ? Sh[b * 5 * R + q * R + r] : bh[q * R + r]);
+    float cn, hn;
+    nn_lstm_cell(s[r], s[R + r], s[2 * R + r], s[3 * R + r], s[4 * R + r], Cprev ? Cprev[i] : 0.f, &cn, &hn);
+    C[i] = cn;
+    H[i] = hn;
 }
 
 // one block per row: LP = log_softmax(Z) (nets.py:202), P = exp(LP)
@@ -292,10 +294,11 @@ __global__ void sens_cell_bwd(const float* dH, float* dC, const float* S, const 
     const int r = (int)(i % R);
     const int64_t b = kb % Bs, k = kb / Bs;
     const float* s = S + b * 5 * R;
-    const float ig = sigm(s[r]), fg = sigm(s[R + r]), og = sigm(s[2 * R + r]);
-    const float g1 = s[3 * R + r], g2 = s[4 * R + r], g = fmaxf(g1, g2);
+    // the forward's activations as it computed them (nn_lstm_cell)
+    const float ig = nn_sigmoidf(s[r]), fg = nn_sigmoidf(s[R + r]), og = nn_sigmoidf(s[2 * R + r]);
+    const float g1 = s[3 * R + r], g2 = s[4 * R + r], g = g1 > g2 ? g1 : g2;
     const float c = C[b * R + r], cp = Cprev ? Cprev[b * R + r] : 0.f;
-    const float th = tanhf(c);
+    const float th = nn_tanhf(c);
     const float dh = dH[i];
     const float dc = dC[i] + dh * og * (1.f - th * th);
     const float dog = dh * th;
@@ -396,6 +399,7 @@ struct SensWork {
     int64_t D = 0;
     float* X = nullptr;     // [L + 1][Bs, E] cell inputs
     float* S = nullptr;     // [L + 1][Bs, 5R] gate sums
+    float* Sh = nullptr;    // [Bs, 5R] the h2h chain of the current cell
     float* C = nullptr;     // [L + 1][Bs, R]
     float* H = nullptr;     // [L + 1][Bs, R]
     float* Z = nullptr;     // [Bs, V] logits
@@ -414,10 +418,10 @@ struct SensWork {
 namespace {
 
 void free_all(SensWork* w) {
-    float* ps[] = {w->X, w->S, w->C, w->H, w->Z, w->LP, w->P, w->IG, w->SG, w->PW, w->dH, w->dC, w->dS, w->dX, w->part};
+    float* ps[] = {w->X, w->S, w->Sh, w->C, w->H, w->Z, w->LP, w->P, w->IG, w->SG, w->PW, w->dH, w->dC, w->dS, w->dX, w->part};
     for (float* p : ps)
         if (p) (void)hipFree(p);
-    w->X = w->S = w->C = w->H = w->Z = w->LP = w->P = w->IG = w->SG = w->PW = nullptr;
+    w->X = w->S = w->Sh = w->C = w->H = w->Z = w->LP = w->P = w->IG = w->SG = w->PW = nullptr;
     w->dH = w->dC = w->dS = w->dX = w->part = nullptr;
     w->Bs = w->K = w->L = 0;
     w->D = 0;
@@ -428,7 +432,7 @@ hipError_t grow(SensWork* w, const SensParams* p) {
     free_all(w);
     const int64_t L1 = p->L + 1, Bs = p->Bs, K = p->K, E = p->E, R = p->R, V = p->V1;
     const struct { float** q; int64_t n; } a[] = {
-        {&w->X, L1 * Bs * E}, {&w->S, L1 * Bs * 5 * R}, {&w->C, L1 * Bs * R}, {&w->H, L1 * Bs * R},
+        {&w->X, L1 * Bs * E}, {&w->S, L1 * Bs * 5 * R}, {&w->Sh, Bs * 5 * R}, {&w->C, L1 * Bs * R}, {&w->H, L1 * Bs * R},
         {&w->Z, Bs * V}, {&w->LP, Bs * V}, {&w->P, Bs * V}, {&w->IG, Bs * K}, {&w->SG, Bs * K}, {&w->PW, Bs * R},
         {&w->dH, K * Bs * R}, {&w->dC, K * Bs * R}, {&w->dS, K * L1 * Bs * 5 * R}, {&w->dX, K * L1 * Bs * E},
         {&w->part, SENS_NZ * p->D}};
@@ -454,6 +458,17 @@ TileArgs targs(int M, int N, int R, const float* B, int64_t sBk, int64_t sBr, in
     t.C = C; t.sCk = sCk; t.sCm = sCm; t.sCn = sCn;
     t.beta = beta;
     t.k0 = 0; t.kpr = 1; t.k_end = 1;
+    t.bias = nullptr;
+    t.kperm = 0;
+    return t;
+}
+
+// the forward products in the reference's arithmetic: every chain from its bias, r in the nn_kperm order, as the
+// engine's decode (bit-exact with the reference): the activations, and so the max-out choices of the cells, are
+// the reference's own
+TileArgs fwd(TileArgs t, const float* bias) {
+    t.bias = bias;
+    t.kperm = 1;
     return t;
 }
 
@@ -508,22 +523,18 @@ extern "C" int nicnes_sens_run(SensWork* w, const SensParams* p, hipStream_t st)
 
     // ---- forward: image cell, then L token cells (forward_for_sensitivity, nets.py:48-64); C = A B with
     // A row-major [rows, red] and B = W^T of a row-major [out, in] weight
-    gemm(sa(p->fc, 0, F, 1), targs(Bs, E, F, Wimg, 0, 1, F, Xs(0), 0, E, 1), 1, st);          // img_embed
-    hipLaunchKernelGGL(sens_bias_rows, dim3(blocks((int64_t)Bs * E, 256)), dim3(256), 0, st, Xs(0), bimg,
-                       (const float*)nullptr, Bs, E);
+    gemm(sa(p->fc, 0, F, 1), fwd(targs(Bs, E, F, Wimg, 0, 1, F, Xs(0), 0, E, 1), bimg), 1, st);   // img_embed
     for (int i = 0; i <= L; ++i) {
         if (i >= 1)
             hipLaunchKernelGGL(sens_embed_gather, dim3(Bs), dim3(E), 0, st, Xs(i), Wemb, p->tok, p->tok_stride,
                                tok_col(i), Bs, E);
-        gemm(sa(Xs(i), 0, E, 1), targs(Bs, G5, E, Wi, 0, 1, E, Ss(i), 0, G5, 1), 1, st);          // i2h
-        if (i >= 1) gemm(sa(Hs(i - 1), 0, R, 1), targs(Bs, G5, R, Wh, 0, 1, R, Ss(i), 0, G5, 1, 1), 1, st);   // h2h
-        hipLaunchKernelGGL(sens_bias_rows, dim3(blocks((int64_t)Bs * G5, 256)), dim3(256), 0, st, Ss(i), bi, bh, Bs, G5);
+        gemm(sa(Xs(i), 0, E, 1), fwd(targs(Bs, G5, E, Wi, 0, 1, E, Ss(i), 0, G5, 1), bi), 1, st);          // i2h
+        if (i >= 1) gemm(sa(Hs(i - 1), 0, R, 1), fwd(targs(Bs, G5, R, Wh, 0, 1, R, w->Sh, 0, G5, 1), bh), 1, st);   // h2h
         hipLaunchKernelGGL(sens_cell_fwd, dim3(blocks((int64_t)Bs * R, 256)), dim3(256), 0, st, Ss(i),
+                           i ? (const float*)w->Sh : (const float*)nullptr, bh,
                            i ? (const float*)Cs(i - 1) : (const float*)nullptr, Cs(i), Hs(i), Bs, R);
     }
-    gemm(sa(Hs(L), 0, R, 1), targs(Bs, V, R, Wl, 0, 1, R, w->Z, 0, V, 1), 1, st);               // logit
-    hipLaunchKernelGGL(sens_bias_rows, dim3(blocks((int64_t)Bs * V, 256)), dim3(256), 0, st, w->Z, bl,
-                       (const float*)nullptr, Bs, V);
+    gemm(sa(Hs(L), 0, R, 1), fwd(targs(Bs, V, R, Wl, 0, 1, R, w->Z, 0, V, 1), bl), 1, st);             // logit
     hipLaunchKernelGGL(sens_logsoftmax, dim3(Bs), dim3(256), 0, st, w->Z, w->LP, w->P, V);
 
     // ---- the K backward passes at once
@@ -538,6 +549,12 @@ extern "C" int nicnes_sens_run(SensWork* w, const SensParams* p, hipStream_t st)
     gemm(sa(w->P, 0, V, 1), targs(Bs, R, V, Wl, 0, R, 1, w->PW, 0, R, 1), 1, st);
     hipLaunchKernelGGL(sens_dh_logit, dim3(Bs, K), dim3(R), 0, st, w->LP, w->IG, w->SG, w->PW, Wl, w->dH, Bs, V, K, R,
                        p->split);
+    static const int dump = getenv("NICNES_SENS_DUMP") ? atoi(getenv("NICNES_SENS_DUMP")) : 0;   // dev: intermediates
+    if (dump == 1) return hipMemcpyAsync(p->out, w->dH, (size_t)K * Bs * R * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
+    if (dump == 6) return hipMemcpyAsync(p->out, w->LP, (size_t)Bs * V * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
+    if (dump == 7) return hipMemcpyAsync(p->out, w->IG, (size_t)Bs * K * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
+    if (dump == 8) return hipMemcpyAsync(p->out, w->SG, (size_t)Bs * K * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
+    if (dump == 4) return hipMemcpyAsync(p->out, w->PW, (size_t)Bs * R * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
     if (hipMemsetAsync(w->dC, 0, (size_t)K * Bs * R * sizeof(float), st) != hipSuccess) return 4;
     const int64_t sdk = L1 * Bs * G5, sxk = L1 * Bs * E;
     for (int i = L; i >= 0; --i) {
@@ -548,6 +565,22 @@ extern "C" int nicnes_sens_run(SensWork* w, const SensParams* p, hipStream_t st)
         gemm(sa(dSi, sdk, G5, 1), targs(Bs, E, G5, Wi, 0, E, 1, w->dX + (int64_t)i * Bs * E, sxk, E, 1), K, st);
         if (i >= 1)
             gemm(sa(dSi, sdk, G5, 1), targs(Bs, R, G5, Wh, 0, R, 1, w->dH, (int64_t)Bs * R, R, 1), K, st);
+        static const int dcell = getenv("NICNES_SENS_CELL") ? atoi(getenv("NICNES_SENS_CELL")) : L;
+        if (dump == 2 && i == dcell) {   // dS of cell dcell, [K][Bs][5R] (strided rows copied one k at a time)
+            for (int k = 0; k < K; ++k)
+                if (hipMemcpyAsync(p->out + (int64_t)k * Bs * G5, dSi + k * sdk, (size_t)Bs * G5 * sizeof(float),
+                                   hipMemcpyDeviceToDevice, st)) return 7;
+            return 0;
+        }
+        if (dump == 3 && i == dcell) {   // dX of cell dcell, [K][Bs][E]
+            for (int k = 0; k < K; ++k)
+                if (hipMemcpyAsync(p->out + (int64_t)k * Bs * E, w->dX + (int64_t)i * Bs * E + k * sxk, (size_t)Bs * E * sizeof(float),
+                                   hipMemcpyDeviceToDevice, st)) return 7;
+            return 0;
+        }
+        if (dump == 5 && i == dcell) {   // dH fed to cell dcell - 1, [K][Bs][R]
+            return hipMemcpyAsync(p->out, w->dH, (size_t)K * Bs * R * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
+        }
     }
     // gate weights: G_k[g, e] = sum over (cell i, b) of dS_k[i, b, g] X_i[b, e] (h2h: cells 1..L with H_{i-1})
     sqsum(sa(w->dS, sdk, 1, G5), targs(G5, E, (int)(L1 * Bs), w->X, 0, E, 1, part + p->off_i2h_w, D, E, 1), K, SENS_NZ, st);
