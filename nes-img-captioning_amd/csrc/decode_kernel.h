@@ -34,7 +34,7 @@ struct DecodeParams {
     uint32_t test_stall_ms;      // test hook (NICNES_TEST_COOP_STALL): coop workgroup 0 starts this late, past the
                                  // partners' spin bound, so they time out (0 = off)
     int32_t no_exit;             // 1: no per-slab early exit (log-probs of a multi-slab batch, see below)
-    int32_t no_mask;             // 1 (fused path): feed every argmax back unmasked (forward_for_sensitivity)
+    int32_t no_mask;             // 1: feed every argmax back unmasked (forward_for_sensitivity); fused, split, coop
     int32_t force_exact;         // test hook (NICNES_FORCE_EXACT=1): every step takes the exact tie pass
     float lse_margin;            // widening of the bounded-lse interval: 2e-3 (test hook NICNES_LSE_MARGIN)
     int32_t bounded_lse;         // 1: greedy-only decode with the pair-bounded lse (needs lp == NULL)

@@ -833,12 +833,17 @@ struct SampleStage {
         const uint64_t pb = __builtin_bit_cast(uint64_t, P);
         const u32x4 w = {(uint32_t)pb, (uint32_t)(pb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
         __builtin_amdgcn_raw_buffer_store_b128(w, slot, (int)vo, (int)(so + 8u * 1024u), SLOG_STORE_POLICY);
+        asm volatile("s_nop 1" ::"v"(w));                // (the wait states of the block record below)
         if ((s % SLOG_BLOCK) == SLOG_BLOCK - 1 || s == nst - 1) {      // the block's record (wave-uniform branch)
             const uint64_t bb = __builtin_bit_cast(uint64_t, Bk);
             const u32x4 wb = {(uint32_t)bb, (uint32_t)(bb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
             __builtin_amdgcn_raw_buffer_store_b128(wb, slot, (int)vb,
                                                    (int)(SLOG_STAGE_BYTES * (uint32_t)nst + SLOG_BLK_BYTES * (uint32_t)(s / SLOG_BLOCK)),
                                                    SLOG_STORE_POLICY);
+            // the 16-byte store reads its data registers after issue: the compiler put the zeroing of Bk right
+            // behind it with no wait state and lanes 12-15 of each 16 stored 0 (gfx950, measured); the asm keeps
+            // Bk's registers unwritten for two wait states
+            asm volatile("s_nop 1" : "+v"(Bk));
             Bk = 0.0;
         }
     }
@@ -925,6 +930,9 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
         const uint32_t vb = 16u * (uint32_t)(threadIdx.x & 63) + 1024u * (uint32_t)(threadIdx.x >> 6);
         int qf = -1;
         double cq = 0.0, cl = 0.0;
+#ifdef SAMPLE_BLOCK_CHECK
+        double sblk = 0.0;
+#endif
         for (int q0 = 0; q0 < nblk; q0 += 10) {
             // B and r as their own loads (a 16-byte load narrowed by the compiler returned B's low word as r)
             double Bw[10];
@@ -941,9 +949,29 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
                     const double a = samp_scale(Bw[j], rw[j] - R);
                     const double ao = __shfl_xor(a, 32);
                     const double S = hh == 0 ? a + ao : ao + a;
+#ifdef SAMPLE_BLOCK_CHECK
+                    {
+                        const int q = q0 + j, qa = SLOG_BLOCK * q, qn = min(SLOG_BLOCK, nst - qa);
+                        double tot = 0.0;
+                        for (int i = 0; i < qn; ++i) {
+                            const uint32_t o = vo + SLOG_STAGE_BYTES * (uint32_t)(qa + i) + 8u * 1024u;
+                            const double P = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lr, (int)o, 0, 16));
+                            const float r = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (int)o + 8, 0, 16));
+                            tot += samp_scale(P, r - R);
+                        }
+                        const double a0 = samp_scale(Bw[j], rw[j] - R);
+                        if (fabs(tot - a0) > 1e-9 * fabs(tot))
+                            printf("BLKCHK blk %d nblk %d lane %d wave %d qf %d Sblk %.17g stages %.17g r %g R %g\n", q, nblk,
+                                   (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), qf, a0, tot, rw[j], R);
+                    }
+#endif
                     if (qf < 0) {
-                        if (cum + S > thr) { qf = q0 + j; cq = cum; }
-                        else { cl = cum; cum += S; }
+                        if (cum + S > thr) {
+                            qf = q0 + j; cq = cum;
+#ifdef SAMPLE_BLOCK_CHECK
+                            sblk = S;
+#endif
+                        } else { cl = cum; cum += S; }
                     }
                 }
             }
@@ -974,6 +1002,17 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
             }
         }
         if (!have) { sf = sa + sn - 1; cb = csl; rf = rl; }     // the block's stage sums stop short: its last stage
+#ifdef SAMPLE_BLOCK_CHECK
+        {   // dev: the block record against the sum of its stage records
+            double tot = 0.0;
+            for (int j = 0; j < SLOG_BLOCK; ++j) {
+                const double a = samp_scale(Pw[j], rw[j] - R);
+                const double ao = __shfl_xor(a, 32);
+                if (j < sn) tot += hh == 0 ? a + ao : ao + a;
+            }
+            if (hh == 0 && fabs(tot - sblk) > 1e-9 * fabs(tot)) atomicAdd(p.stats + 1, 1000);
+        }
+#endif
         f32x16 x0, x1;
         samp_load_stage(lr, vo, SLOG_STAGE_BYTES * (uint32_t)sf, x0, x1);
         sample_stage_walk(x0, x1, sf, hh, rf, __builtin_ldexp(1.0, (int)fmaxf(rf - R, -2000.f)), m, lse, thr, cb, found,
@@ -1912,7 +1951,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_cell_kernel(DecodePara
         const bool prev_unf = t == 1 || p.seq[o - 1] != 0;
 #endif
         const bool unfinished = prev_unf && tok > 0;
-        it = unfinished ? tok : 0;
+        it = (unfinished || p.no_mask) ? tok : 0;
 #if !DECODE_PROF
         if (c.q == 0 && folder && c.hh == 0 && c.row_valid) {
             p.seq[o] = it;
@@ -2196,7 +2235,7 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         }
         if (tok >= p.V1) tok = 0;               // every logit NaN: end the caption (fused kernel rule)
         const bool unfinished = unf_prev != 0.f && tok > 0;
-        it = unfinished ? tok : 0;
+        it = (unfinished || p.no_mask) ? tok : 0;
         st1(c.scr_r, lo, U_SLOT, unfinished ? 1.f : 0.f);
 #if !DECODE_PROF
         if (q == 0 && c.hh == 0 && c.row_valid) {

@@ -43,7 +43,7 @@ namespace {
 // out[z][m, n] = sum over the range (sq partials, summed over ranges by sens_finish).
 #define TM 64
 #define TN 64
-#define TR 16
+#define TR 32
 #define LDS_P (TM + 1)
 
 struct Strided {             // element (k, m, r) at p + k sk + m sm + r sr
@@ -85,42 +85,46 @@ struct TileArgs {
 // nn_kperm inside a 16-aligned chunk: chain position p -> r (the 32-wide pattern keeps each half in its 16)
 __device__ __forceinline__ int perm16(int p) { const int j = p >> 1; return (j & 3) + 8 * (j >> 2) + 4 * (p & 1); }
 
-// chunk [r0, r0 + TR) of A (TM rows from m0) and B (TN columns from n0) into registers: 4 + 4 values per
-// thread, the 256 threads laid along the operand's unit-stride dimension
+// chunk [r0, r0 + TR) of A (TM rows from m0) and B (TN columns from n0) into registers: NPT + NPT values per
+// thread, the 256 threads laid along the operand's unit-stride dimension; with kperm, chain position p of the
+// chunk holds r0 + (p & 16) + perm16(p & 15)
+#define NPT (TM * TR / 256)
+__device__ __forceinline__ int chunk_r(const TileArgs& t, int p) { return t.kperm ? (p & 16) + perm16(p & 15) : p; }
+
 template <class AOp>
-__device__ __forceinline__ void tile_load(const AOp& A, const TileArgs& t, int k, int m0, int n0, int r0, float (&ra)[4],
-                                          float (&rb)[4]) {
+__device__ __forceinline__ void tile_load(const AOp& A, const TileArgs& t, int k, int m0, int n0, int r0, float (&ra)[NPT],
+                                          float (&rb)[NPT]) {
     const int tid = threadIdx.x;
     const bool am = A.m_unit();
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < NPT; ++e) {
         const int i = tid + 256 * e;
-        const int m = am ? (i & (TM - 1)) : (i >> 4), r = am ? (i >> 6) : (i & (TR - 1));
-        const int gm = m0 + m, gr = r0 + (t.kperm ? perm16(r) : r);
+        const int m = am ? (i & (TM - 1)) : (i / TR), p = am ? (i / TM) : (i & (TR - 1));
+        const int gm = m0 + m, gr = r0 + chunk_r(t, p);
         ra[e] = (gm < t.M && gr < t.R) ? A(k, gm, gr) : 0.f;
     }
     const bool bn = t.sBn == 1;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < NPT; ++e) {
         const int i = tid + 256 * e;
-        const int n = bn ? (i & (TN - 1)) : (i >> 4), r = bn ? (i >> 6) : (i & (TR - 1));
-        const int gn = n0 + n, gr = r0 + (t.kperm ? perm16(r) : r);
+        const int n = bn ? (i & (TN - 1)) : (i / TR), p = bn ? (i / TN) : (i & (TR - 1));
+        const int gn = n0 + n, gr = r0 + chunk_r(t, p);
         rb[e] = (gn < t.N && gr < t.R) ? t.B[(int64_t)k * t.sBk + (int64_t)gr * t.sBr + (int64_t)gn * t.sBn] : 0.f;
     }
 }
 
 template <class AOp>
-__device__ __forceinline__ void tile_store(const AOp& A, const TileArgs& t, float* As, float* Bs, const float (&ra)[4],
-                                           const float (&rb)[4]) {
+__device__ __forceinline__ void tile_store(const AOp& A, const TileArgs& t, float* As, float* Bs, const float (&ra)[NPT],
+                                           const float (&rb)[NPT]) {
     const int tid = threadIdx.x;
     const bool am = A.m_unit(), bn = t.sBn == 1;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < NPT; ++e) {
         const int i = tid + 256 * e;
-        const int m = am ? (i & (TM - 1)) : (i >> 4), r = am ? (i >> 6) : (i & (TR - 1));
-        As[r * LDS_P + m] = ra[e];
-        const int n = bn ? (i & (TN - 1)) : (i >> 4), rr = bn ? (i >> 6) : (i & (TR - 1));
-        Bs[rr * LDS_P + n] = rb[e];
+        const int m = am ? (i & (TM - 1)) : (i / TR), p = am ? (i / TM) : (i & (TR - 1));
+        As[p * LDS_P + m] = ra[e];
+        const int n = bn ? (i & (TN - 1)) : (i / TR), q = bn ? (i / TN) : (i & (TR - 1));
+        Bs[q * LDS_P + n] = rb[e];
     }
 }
 
@@ -130,7 +134,7 @@ __device__ __forceinline__ void tile_product(const AOp& A, const TileArgs& t, in
                                              f32x16& acc) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wm = 32 * (w >> 1), wn = 32 * (w & 1), kh = lane >> 5, li = lane & 31;
-    float ra[4], rb[4];
+    float ra[NPT], rb[NPT];
     tile_load(A, t, k, m0, n0, 0, ra, rb);
     for (int r0 = 0; r0 < t.R; r0 += TR) {
         __syncthreads();                                     // the previous chunk has been read
@@ -312,59 +316,102 @@ __global__ void sens_cell_bwd(const float* dH, float* dC, const float* S, const 
     dC[i] = dc * fg;
 }
 
-// out[c] = sum_k (sum_{r < rows} X[k sk + r sr + c])^2 (a bias gradient's square sum over the K seeds);
-// out2 (nullable) gets the same
-__global__ void sens_colsum_sq(const float* X, int rows, int cols, int64_t sr, int64_t sk, int K, float* out,
-                               float* out2) {
+// sums[k][c] = sum_{r < rows} X[k sk + r sr + c] (a bias gradient for each of the K seeds): block (64 columns, k),
+// 4 row groups summed in a fixed order
+__global__ __launch_bounds__(256) void sens_colsum_k(const float* X, int rows, int cols, int64_t sr, int64_t sk,
+                                                     float* sums) {
+    __shared__ float red[4][64];
+    const int cl = threadIdx.x & 63, g = threadIdx.x >> 6, k = blockIdx.y;
+    const int c = blockIdx.x * 64 + cl;
+    float s = 0.f;
+    if (c < cols) {
+        const float* x = X + (int64_t)k * sk + c;
+        for (int r = g; r < rows; r += 4) s += x[(int64_t)r * sr];
+    }
+    red[g][cl] = s;
+    __syncthreads();
+    if (g == 0 && c < cols) sums[(int64_t)k * cols + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+}
+
+// out[c] = sum_k sums[k][c]^2 (out2, nullable, gets the same)
+__global__ void sens_sq_over_k(const float* sums, int cols, int K, float* out, float* out2) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= cols) return;
     float sq = 0.f;
     for (int k = 0; k < K; ++k) {
-        const float* x = X + (int64_t)k * sk + c;
-        float s = 0.f;
-        for (int r = 0; r < rows; ++r) s += x[(int64_t)r * sr];
-        sq += s * s;
+        const float v = sums[(int64_t)k * cols + c];
+        sq += v * v;
     }
     out[c] = sq;
     if (out2) out2[c] = sq;
 }
 
-// logit.bias: out[v] = sum_k (sum_b dZ[k, b, v])^2
-__global__ void sens_logb_sq(DzA A, int Bs, float* out) {
+// logit.bias: out[v] = sum_k (sum_b dZ_k[b, v])^2 with sum_b dZ_k[b, v] = [k = group(v)] sum_b lp[b, v] inv_g[b, k]
+// - PS[v, k], PS = p^T S (a tile product)
+__global__ void sens_logb_sq(const float* LP, const float* IG, const float* PS, int Bs, int V, int K, int split,
+                             float* out) {
     const int v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= A.V) return;
+    if (v >= V) return;
+    const int kv = v / split;
+    float own = 0.f;
+    for (int b = 0; b < Bs; ++b) own += LP[(int64_t)b * V + v] * IG[b * K + kv];
     float sq = 0.f;
-    for (int k = 0; k < A.K; ++k) {
-        float s = 0.f;
-        for (int b = 0; b < Bs; ++b) s += A(k, v, b);
-        sq += s * s;
+    for (int k = 0; k < K; ++k) {
+        const float g = (k == kv ? own : 0.f) - PS[(int64_t)v * K + k];
+        sq += g * g;
     }
     out[v] = sq;
 }
 
+// PW = sum over the split partials (fixed order)
+__global__ void sens_sum_parts(const float* parts, int nparts, int64_t n, float* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int z = 0; z < nparts; ++z) s += parts[(int64_t)z * n + i];
+    out[i] = s;
+}
+
 // embedding rows: row t gathers dX of every (cell i >= 1, row b) fed token t (BOS at cell 1, else the greedy
-// token of logit step i - 1), out[t E + e] = sum_k (sum over those (i, b) in order of dX[k, i, b, e])^2.
-// Block p = (i - 1) Bs + b handles the token of pair p if p is its first pair; thread e. dX_all [K][L + 1][Bs][E].
-__global__ void sens_emb_sq(const float* dX, const int32_t* tok, int stride, int L, int Bs, int E, int K, float* out) {
-    const int p = blockIdx.x, e = threadIdx.x;
+// token of logit step i - 1), G_k[t, e] = sum over those (i, b), in order, of dX[k, i, b, e]. Block (p, kc), with
+// pair p = (i - 1) Bs + b: if p is its token's first pair, the token's pairs are listed in LDS and the block adds
+// G_k[t, e]^2 over k in range kc into out[kc][t E + e] (thread e; partial rows summed by sens_finish).
+// dX_all [K][L + 1][Bs][E]; npair <= EMB_MAXP.
+#define EMB_MAXP 4096
+#define EMB_KC 8
+__global__ __launch_bounds__(256) void sens_emb_sq(const float* dX, const int32_t* tok, int stride, int L, int Bs, int E,
+                                                   int K, int64_t D, float* out) {
+    __shared__ int tq[EMB_MAXP];
+    __shared__ int list[EMB_MAXP];
+    __shared__ int cnt;
+    const int p = blockIdx.x, kc = blockIdx.y, e = threadIdx.x;
     const int npair = L * Bs;
-    auto token = [&](int q) {
+    for (int q = threadIdx.x; q < npair; q += blockDim.x) {
         const int i = q / Bs + 1, b = q % Bs;
-        return i == 1 ? 0 : tok[(int64_t)b * stride + (i - 2)];
-    };
-    const int t = token(p);
-    for (int q = 0; q < p; ++q)
-        if (token(q) == t) return;                            // not the first pair of this token
+        tq[q] = i == 1 ? 0 : tok[(int64_t)b * stride + (i - 2)];
+    }
+    __syncthreads();
+    const int t = tq[p];
+    int earlier = 0;
+    for (int q = threadIdx.x; q < p; q += blockDim.x) earlier |= tq[q] == t;
+    if (__syncthreads_or(earlier)) return;                   // not the first pair of this token
+    if (threadIdx.x == 0) {
+        int n = 0;
+        for (int q = p; q < npair; ++q)
+            if (tq[q] == t) list[n++] = (q / Bs + 1) * Bs + q % Bs;    // (cell, row) -> row of dX_all
+        cnt = n;
+    }
+    __syncthreads();
     if (e >= E) return;
     const int64_t sk = (int64_t)(L + 1) * Bs * E;
+    const int kpr = (K + EMB_KC - 1) / EMB_KC, k0 = kc * kpr, k1 = min(k0 + kpr, K);
     float sq = 0.f;
-    for (int k = 0; k < K; ++k) {
+    for (int k = k0; k < k1; ++k) {
         float s = 0.f;
-        for (int q = p; q < npair; ++q)
-            if (token(q) == t) s += dX[(int64_t)k * sk + ((int64_t)(q / Bs + 1) * Bs + q % Bs) * E + e];
+        for (int j = 0; j < cnt; ++j) s += dX[(int64_t)k * sk + (int64_t)list[j] * E + e];
         sq += s * s;
     }
-    out[(int64_t)t * E + e] = sq;
+    out[(int64_t)kc * D + (int64_t)t * E + e] = sq;
 }
 
 // s_j = sqrt(sum over the segment's range partials of part[z][j]) / Bs, then s < underflow -> underflow,
@@ -408,6 +455,9 @@ struct SensWork {
     float* IG = nullptr;    // [Bs, K]
     float* SG = nullptr;    // [Bs, K]
     float* PW = nullptr;    // [Bs, R] p Wl
+    float* PWp = nullptr;   // [32][Bs, R] its split partials
+    float* PS = nullptr;    // [V, K] p^T S
+    float* CS = nullptr;    // [K, 5R] per-seed bias column sums
     float* dH = nullptr;    // [K, Bs, R]
     float* dC = nullptr;    // [K, Bs, R]
     float* dS = nullptr;    // [K][L + 1][Bs][5R]
@@ -418,10 +468,10 @@ struct SensWork {
 namespace {
 
 void free_all(SensWork* w) {
-    float* ps[] = {w->X, w->S, w->Sh, w->C, w->H, w->Z, w->LP, w->P, w->IG, w->SG, w->PW, w->dH, w->dC, w->dS, w->dX, w->part};
+    float* ps[] = {w->X, w->S, w->Sh, w->C, w->H, w->Z, w->LP, w->P, w->IG, w->SG, w->PW, w->PWp, w->PS, w->CS, w->dH, w->dC, w->dS, w->dX, w->part};
     for (float* p : ps)
         if (p) (void)hipFree(p);
-    w->X = w->S = w->Sh = w->C = w->H = w->Z = w->LP = w->P = w->IG = w->SG = w->PW = nullptr;
+    w->X = w->S = w->Sh = w->C = w->H = w->Z = w->LP = w->P = w->IG = w->SG = w->PW = w->PWp = w->PS = w->CS = nullptr;
     w->dH = w->dC = w->dS = w->dX = w->part = nullptr;
     w->Bs = w->K = w->L = 0;
     w->D = 0;
@@ -433,7 +483,7 @@ hipError_t grow(SensWork* w, const SensParams* p) {
     const int64_t L1 = p->L + 1, Bs = p->Bs, K = p->K, E = p->E, R = p->R, V = p->V1;
     const struct { float** q; int64_t n; } a[] = {
         {&w->X, L1 * Bs * E}, {&w->S, L1 * Bs * 5 * R}, {&w->Sh, Bs * 5 * R}, {&w->C, L1 * Bs * R}, {&w->H, L1 * Bs * R},
-        {&w->Z, Bs * V}, {&w->LP, Bs * V}, {&w->P, Bs * V}, {&w->IG, Bs * K}, {&w->SG, Bs * K}, {&w->PW, Bs * R},
+        {&w->Z, Bs * V}, {&w->LP, Bs * V}, {&w->P, Bs * V}, {&w->IG, Bs * K}, {&w->SG, Bs * K}, {&w->PW, Bs * R}, {&w->PWp, 32 * Bs * R}, {&w->PS, V * K}, {&w->CS, K * 5 * R},
         {&w->dH, K * Bs * R}, {&w->dC, K * Bs * R}, {&w->dS, K * L1 * Bs * 5 * R}, {&w->dX, K * L1 * Bs * E},
         {&w->part, SENS_NZ * p->D}};
     for (const auto& x : a) {
@@ -507,6 +557,7 @@ extern "C" void nicnes_sens_destroy(SensWork* w) {
 extern "C" int nicnes_sens_run(SensWork* w, const SensParams* p, hipStream_t st) {
     if (!w || !p || p->Bs < 1 || p->L < 1 || p->split < 1) return 1;
     if (p->E > 256 || p->R > 256) return 1;                     // thread-per-column kernels
+    if ((int64_t)p->L * p->Bs > EMB_MAXP) return 1;             // sens_emb_sq's pair list
     if (grow(w, p) != hipSuccess) return 3;
     const int Bs = p->Bs, E = p->E, R = p->R, F = p->F, V = p->V1, K = p->K, L = p->L, G5 = 5 * R;
     const int64_t D = p->D, L1 = L + 1;
@@ -544,9 +595,21 @@ extern "C" int nicnes_sens_run(SensWork* w, const SensParams* p, hipStream_t st)
     float* part = w->part;
     // logit.weight: G_k[v, r] = sum_b dZ_k[b, v] H_L[b, r]; logit.bias
     sqsum(dz, targs(V, R, Bs, Hs(L), 0, R, 1, part + p->off_log_w, D, R, 1), K, SENS_NZ, st);
-    hipLaunchKernelGGL(sens_logb_sq, dim3(blocks(V, 256)), dim3(256), 0, st, dz, Bs, part + p->off_log_b);
-    // dH of the last cell: p Wl once, then the group terms
-    gemm(sa(w->P, 0, V, 1), targs(Bs, R, V, Wl, 0, R, 1, w->PW, 0, R, 1), 1, st);
+    // logit.bias: PS = p^T S over the batch, then the group terms
+    gemm(sa(w->P, 0, 1, V), targs(V, K, Bs, w->SG, 0, K, 1, w->PS, 0, K, 1), 1, st);
+    hipLaunchKernelGGL(sens_logb_sq, dim3(blocks(V, 256)), dim3(256), 0, st, w->LP, w->IG, w->PS, Bs, V, K, p->split,
+                       part + p->off_log_b);
+    // dH of the last cell: p Wl once (split over the vocabulary: nsp partial products, summed in order), then the
+    // group terms
+    {
+        int nsp = 1;
+        for (int d = 32; d > 1; --d)
+            if (V % d == 0 && V / d >= TR) { nsp = d; break; }
+        const int cl = V / nsp;
+        gemm(sa(w->P, cl, V, 1), targs(Bs, R, cl, Wl, (int64_t)cl * R, R, 1, w->PWp, (int64_t)Bs * R, R, 1), nsp, st);
+        hipLaunchKernelGGL(sens_sum_parts, dim3(blocks((int64_t)Bs * R, 256)), dim3(256), 0, st, w->PWp, nsp,
+                           (int64_t)Bs * R, w->PW);
+    }
     hipLaunchKernelGGL(sens_dh_logit, dim3(Bs, K), dim3(R), 0, st, w->LP, w->IG, w->SG, w->PW, Wl, w->dH, Bs, V, K, R,
                        p->split);
     static const int dump = getenv("NICNES_SENS_DUMP") ? atoi(getenv("NICNES_SENS_DUMP")) : 0;   // dev: intermediates
@@ -587,22 +650,27 @@ extern "C" int nicnes_sens_run(SensWork* w, const SensParams* p, hipStream_t st)
     sqsum(sa(w->dS + (int64_t)Bs * G5, sdk, 1, G5), targs(G5, R, L * Bs, w->H, 0, R, 1, part + p->off_h2h_w, D, R, 1), K,
           SENS_NZ, st);
     // both gate biases take every cell's dS (h2h's bias is added at cell 0 too, where h = 0)
-    hipLaunchKernelGGL(sens_colsum_sq, dim3(blocks(G5, 256)), dim3(256), 0, st, w->dS, (int)(L1 * Bs), G5, (int64_t)G5,
-                       sdk, K, part + p->off_i2h_b, part + p->off_h2h_b);
+    hipLaunchKernelGGL(sens_colsum_k, dim3(blocks(G5, 64), K), dim3(256), 0, st, w->dS, (int)(L1 * Bs), G5, (int64_t)G5,
+                       sdk, w->CS);
+    hipLaunchKernelGGL(sens_sq_over_k, dim3(blocks(G5, 256)), dim3(256), 0, st, w->CS, G5, K, part + p->off_i2h_b,
+                       part + p->off_h2h_b);
     // img_embed: G_k[e, f] = sum_b dX_k[0, b, e] fc[b, f]; its bias
     sqsum(sa(w->dX, sxk, 1, E), targs(E, F, Bs, p->fc, 0, F, 1, part + p->off_img_w, D, F, 1), K, SENS_NZ, st);
-    hipLaunchKernelGGL(sens_colsum_sq, dim3(blocks(E, 256)), dim3(256), 0, st, w->dX, Bs, E, (int64_t)E, sxk, K,
-                       part + p->off_img_b, (float*)nullptr);
-    // embedding rows never fed stay 0
-    if (hipMemsetAsync(part + p->off_emb_w, 0, (size_t)(p->off_log_w - p->off_emb_w) * sizeof(float), st) != hipSuccess)
-        return 4;
-    hipLaunchKernelGGL(sens_emb_sq, dim3(L * Bs), dim3(E), 0, st, w->dX, p->tok, p->tok_stride, L, Bs, E, K,
+    hipLaunchKernelGGL(sens_colsum_k, dim3(blocks(E, 64), K), dim3(256), 0, st, w->dX, Bs, E, (int64_t)E, sxk, w->CS);
+    hipLaunchKernelGGL(sens_sq_over_k, dim3(blocks(E, 256)), dim3(256), 0, st, w->CS, E, K, part + p->off_img_b,
+                       (float*)nullptr);
+    // embedding rows never fed stay 0 (in every partial row)
+    for (int z = 0; z < EMB_KC; ++z)
+        if (hipMemsetAsync(part + (int64_t)z * D + p->off_emb_w, 0, (size_t)(p->off_log_w - p->off_emb_w) * sizeof(float),
+                           st) != hipSuccess)
+            return 4;
+    hipLaunchKernelGGL(sens_emb_sq, dim3(L * Bs, EMB_KC), dim3(256), 0, st, w->dX, p->tok, p->tok_stride, L, Bs, E, K, D,
                        part + p->off_emb_w);
     Segs sg;
     const int64_t offs[10] = {p->off_img_w, p->off_img_b, p->off_emb_w, p->off_log_w, p->off_log_b,
                               p->off_i2h_w, p->off_i2h_b, p->off_h2h_w, p->off_h2h_b, D};
     const int kpr = (K + SENS_NZ - 1) / SENS_NZ, nzk = (K + kpr - 1) / kpr;
-    const int nz[9] = {nzk, 1, 1, nzk, 1, nzk, 1, nzk, 1};     // weights: k-range partials; the rest: one row
+    const int nz[9] = {nzk, 1, EMB_KC, nzk, 1, nzk, 1, nzk, 1};   // k-range partial rows per segment
     for (int q = 0; q < 10; ++q) sg.off[q] = offs[q];
     for (int q = 0; q < 9; ++q) sg.nz[q] = nz[q];
     hipLaunchKernelGGL(sens_finish, dim3(blocks(D, 256)), dim3(256), 0, st, part, D, sg, 1.f / (float)Bs, p->underflow,
