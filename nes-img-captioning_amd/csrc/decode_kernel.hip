@@ -380,7 +380,9 @@ struct NoMid {
 
 // mid() runs before half-chunk MID of the 8 (8: after the last MFMA; 9: never): the logit loop's W+- store
 // of the next stage and the loads of the one after (LOGIT_MIDSTORE)
-template <int MID = 8, class Mid = NoMid>
+// HALF: chain a only (a stage whose rows 32-63 are all padding: acc1 keeps the padding bias, -inf, which is
+// what the skipped products would leave in it)
+template <int MID = 8, bool HALF = false, class Mid = NoMid>
 __device__ __forceinline__ void mfma_stage64_o(const float* w, const float* bias, const float (&Bop)[64], int arow,
                                                int hh, f32x16& acc0, f32x16& acc1, Mid&& mid = Mid()) {
     const float* row0 = w + arow;
@@ -401,13 +403,14 @@ __device__ __forceinline__ void mfma_stage64_o(const float* w, const float* bias
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             a0[c] = *reinterpret_cast<const f32x4*>(row0 + T * 32 + 4 * c);
-            a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
+            if constexpr (!HALF) a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
         }
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) {
             if (jj == 8) at(2 * T + 1);
             acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bop[16 * T + jj], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
+            if constexpr (!HALF)
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
         }
     }
     at(8);
@@ -756,9 +759,22 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
 // loads and then the crossing stage in one
 #define SLOG_BLOCK 8
 #define SLOG_BLK_BYTES 8192u
+#ifndef COOP_HALF_LAST
+#define COOP_HALF_LAST 0         // 1: coop ranges run a last stage of padding rows 32-63 as chain a only (spills
+                                 // 12 VGPRs inside the stage loop at the 256-VGPR budget: not adopted)
+#endif
+#ifndef SAMP_SPLIT_STORES
+#define SAMP_SPLIT_STORES 0      // 1: the late sign's stores after its MFMAs (+2.5 % sampled kernel time, measured)
+#endif
+#ifndef SAMP_EARLY_STORES
+#define SAMP_EARLY_STORES 0      // 1: the early sign's logit stores before its MFMAs
+#endif
+#ifndef SAMP_L1_ROUND
+#define SAMP_L1_ROUND 20         // block records per round of the pick's level 1 (V1 <= 10240: one round)
+#endif
 #define SLOT_SPIN_TICKS 50000000ull   // 0.5 s of s_memrealtime (100 MHz) to find a free logit slot
 #ifndef SLOG_STORE_POLICY
-#define SLOG_STORE_POLICY 0      // cache policy of the slot stores (2: nt, streaming past the L2's normal allocation)
+#define SLOG_STORE_POLICY 2      // cache policy of the slot stores: nt (streaming; -2 % sampled kernel time vs the default, measured)
 #endif
 
 __device__ __forceinline__ float samp_p(float x, float ref) {
@@ -780,14 +796,21 @@ __device__ __forceinline__ double samp_scale(double x, float e) {
 // place of the greedy epilogue
 struct NoHook {
     static constexpr bool replaces = false;
+    static constexpr bool split = false;
+    static constexpr bool early = false;
     __device__ __forceinline__ void operator()(const f32x16&, const f32x16&, int) const {}
+    template <int MODE>
+    __device__ __forceinline__ void part(const f32x16&, const f32x16&, int) const {}
 };
 
 // the sampled decode's logit loop epilogue: running max m, reference r = ceil(m log2e), the lane's running sum T
 // of its terms relative to 2^r; stores the stage's logits and {P, r} to the slot (one wave instruction per
-// 1 KiB word)
+// 1 KiB word). part<1> is the arithmetic, part<2> the stores (`split`: the waves whose epilogue runs before
+// their MFMAs issue the stores after them, behind that stage's staging loads)
 struct SampleStage {
     static constexpr bool replaces = true;
+    static constexpr bool split = SAMP_SPLIT_STORES;
+    static constexpr bool early = SAMP_EARLY_STORES;
     rsrc_t slot;
     uint32_t vo;      // 16 * lane + SLOG_WAVE_BYTES * wave
     uint32_t vb;      // 16 * lane + 1024 * wave (block records)
@@ -796,55 +819,69 @@ struct SampleStage {
     float& ref;
     double& T;
     double& Bk;       // the current block's sum of terms relative to 2^ref
+    double& Pp;       // the stage's own sum (part<1> -> part<2>)
     __device__ __forceinline__ void operator()(const f32x16& q0, const f32x16& q1, int s) const {
+        part<7>(q0, q1, s);
+    }
+    // MODE bit 1: the arithmetic; bit 2: the logit stores; bit 4: the {P, r} and block records
+    template <int MODE>
+    __device__ __forceinline__ void part(const f32x16& q0, const f32x16& q1, int s) const {
         if (s < 0) return;                               // the pipeline's first epilogue: no stage yet
         const uint32_t so = SLOG_STAGE_BYTES * (uint32_t)s;
+        constexpr bool ARITH = (MODE & 1) != 0, STORES = (MODE & 2) != 0, RECS = (MODE & 4) != 0;
 #if !(DECODE_ABLATE & 256)
+        if constexpr (STORES) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const f32x4 a = {q0[4 * k], q0[4 * k + 1], q0[4 * k + 2], q0[4 * k + 3]};
-            const f32x4 b = {q1[4 * k], q1[4 * k + 1], q1[4 * k + 2], q1[4 * k + 3]};
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), slot, (int)vo, (int)(so + 1024u * k), SLOG_STORE_POLICY);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), slot, (int)vo, (int)(so + 1024u * (4 + k)), SLOG_STORE_POLICY);
+            for (int k = 0; k < 4; ++k) {
+                const f32x4 a = {q0[4 * k], q0[4 * k + 1], q0[4 * k + 2], q0[4 * k + 3]};
+                const f32x4 b = {q1[4 * k], q1[4 * k + 1], q1[4 * k + 2], q1[4 * k + 3]};
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), slot, (int)vo, (int)(so + 1024u * k), SLOG_STORE_POLICY);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), slot, (int)vo, (int)(so + 1024u * (4 + k)), SLOG_STORE_POLICY);
+            }
         }
 #endif
-        const float mnew = vmax2(m, vmax2(vmax16(q0), vmax16(q1)));
-        const float rnew = ceilf(mnew * LOG2E);
-        if (rnew > ref) {
-            T = samp_scale(T, ref - rnew);
-            Bk = samp_scale(Bk, ref - rnew);
-            ref = rnew;
-        }
-        m = mnew;
-        double P = 0.0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float qa[4], qb[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                qa[e] = samp_p(q0[4 * k + e], ref);
-                qb[e] = samp_p(q1[4 * k + e], ref);
+        if constexpr (ARITH) {
+            const float mnew = vmax2(m, vmax2(vmax16(q0), vmax16(q1)));
+            const float rnew = ceilf(mnew * LOG2E);
+            if (rnew > ref) {
+                T = samp_scale(T, ref - rnew);
+                Bk = samp_scale(Bk, ref - rnew);
+                ref = rnew;
             }
-            P += (double)samp_group(qa);
-            P += (double)samp_group(qb);
+            m = mnew;
+            double P = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float qa[4], qb[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    qa[e] = samp_p(q0[4 * k + e], ref);
+                    qb[e] = samp_p(q1[4 * k + e], ref);
+                }
+                P += (double)samp_group(qa);
+                P += (double)samp_group(qb);
+            }
+            T += P;
+            Bk += P;
+            Pp = P;
         }
-        T += P;
-        Bk += P;
-        const uint64_t pb = __builtin_bit_cast(uint64_t, P);
-        const u32x4 w = {(uint32_t)pb, (uint32_t)(pb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
-        __builtin_amdgcn_raw_buffer_store_b128(w, slot, (int)vo, (int)(so + 8u * 1024u), SLOG_STORE_POLICY);
-        asm volatile("s_nop 1" ::"v"(w));                // (the wait states of the block record below)
-        if ((s % SLOG_BLOCK) == SLOG_BLOCK - 1 || s == nst - 1) {      // the block's record (wave-uniform branch)
-            const uint64_t bb = __builtin_bit_cast(uint64_t, Bk);
-            const u32x4 wb = {(uint32_t)bb, (uint32_t)(bb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
-            __builtin_amdgcn_raw_buffer_store_b128(wb, slot, (int)vb,
-                                                   (int)(SLOG_STAGE_BYTES * (uint32_t)nst + SLOG_BLK_BYTES * (uint32_t)(s / SLOG_BLOCK)),
-                                                   SLOG_STORE_POLICY);
-            // the 16-byte store reads its data registers after issue: the compiler put the zeroing of Bk right
-            // behind it with no wait state and lanes 12-15 of each 16 stored 0 (gfx950, measured); the asm keeps
-            // Bk's registers unwritten for two wait states
-            asm volatile("s_nop 1" : "+v"(Bk));
-            Bk = 0.0;
+        if constexpr (RECS) {
+            const uint64_t pb = __builtin_bit_cast(uint64_t, Pp);
+            const u32x4 w = {(uint32_t)pb, (uint32_t)(pb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
+            __builtin_amdgcn_raw_buffer_store_b128(w, slot, (int)vo, (int)(so + 8u * 1024u), SLOG_STORE_POLICY);
+            asm volatile("s_nop 1" ::"v"(w));                // (the wait states of the block record below)
+            if ((s % SLOG_BLOCK) == SLOG_BLOCK - 1 || s == nst - 1) {      // the block's record (wave-uniform branch)
+                const uint64_t bb = __builtin_bit_cast(uint64_t, Bk);
+                const u32x4 wb = {(uint32_t)bb, (uint32_t)(bb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
+                __builtin_amdgcn_raw_buffer_store_b128(wb, slot, (int)vb,
+                                                       (int)(SLOG_STAGE_BYTES * (uint32_t)nst + SLOG_BLK_BYTES * (uint32_t)(s / SLOG_BLOCK)),
+                                                       SLOG_STORE_POLICY);
+                // the 16-byte store reads its data registers after issue: the compiler put the zeroing of Bk
+                // right behind it with no wait state and lanes 12-15 of each 16 stored 0 (gfx950, measured); the
+                // asm keeps Bk's registers unwritten for two wait states
+                asm volatile("s_nop 1" : "+v"(Bk));
+                Bk = 0.0;
+            }
         }
     }
 };
@@ -905,7 +942,8 @@ __device__ __forceinline__ void samp_load_stage(rsrc_t lr, uint32_t vo, uint32_t
 // that stage / V1 - 1 (stats[1] counts those rows).
 template <bool FULL>
 __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, uint32_t vo, int hh, float m, float lse,
-                                            float R, double thr, int& tok, float& lpv) {
+                                            float R, double thr, int& tok, float& lpv, int pm = 0) {
+    (void)pm;                                            // DECODE_PROF: the step's mark base
     const int nst = (p.V1 + 63) >> 6;
     double cum = 0.0, cb = 0.0;
     bool found = false;
@@ -933,18 +971,18 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
 #ifdef SAMPLE_BLOCK_CHECK
         double sblk = 0.0;
 #endif
-        for (int q0 = 0; q0 < nblk; q0 += 10) {
+        for (int q0 = 0; q0 < nblk; q0 += SAMP_L1_ROUND) {
             // B and r as their own loads (a 16-byte load narrowed by the compiler returned B's low word as r)
-            double Bw[10];
-            float rw[10];
+            double Bw[SAMP_L1_ROUND];
+            float rw[SAMP_L1_ROUND];
 #pragma unroll
-            for (int j = 0; j < 10; ++j) {
+            for (int j = 0; j < SAMP_L1_ROUND; ++j) {
                 const int so = (int)(SLOG_STAGE_BYTES * (uint32_t)nst + SLOG_BLK_BYTES * (uint32_t)min(q0 + j, nblk - 1));
                 Bw[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lr, (int)vb, so, 16));
                 rw[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (int)vb + 8, so, 16));
             }
 #pragma unroll
-            for (int j = 0; j < 10; ++j) {
+            for (int j = 0; j < SAMP_L1_ROUND; ++j) {
                 if (q0 + j < nblk) {
                     const double a = samp_scale(Bw[j], rw[j] - R);
                     const double ao = __shfl_xor(a, 32);
@@ -978,6 +1016,7 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
             if (__all(qf >= 0 ? 1 : 0)) break;
         }
         if (qf < 0) { qf = nblk - 1; cq = cl; }                 // thr at the very end (rounding): the last block
+        PROF_MARK(pm + 22);
         // level 2: the stage records of block qf (a per-lane block: the stage offset goes in the vector offset)
         const int sa = SLOG_BLOCK * qf, sn = min(SLOG_BLOCK, nst - sa);
         double Pw[SLOG_BLOCK];
@@ -1013,6 +1052,7 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
             if (hh == 0 && fabs(tot - sblk) > 1e-9 * fabs(tot)) atomicAdd(p.stats + 1, 1000);
         }
 #endif
+        PROF_MARK(pm + 23);
         f32x16 x0, x1;
         samp_load_stage(lr, vo, SLOG_STAGE_BYTES * (uint32_t)sf, x0, x1);
         sample_stage_walk(x0, x1, sf, hh, rf, __builtin_ldexp(1.0, (int)fmaxf(rf - R, -2000.f)), m, lse, thr, cb, found,
@@ -1054,7 +1094,9 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
     else { tok = other; lpv = olp; }
 }
 
-template <int G, bool PAIRS, class Tail = NoTail, class Hook = NoHook>
+// HALF_LAST: the range's last stage runs chain a only when its rows 32-63 are all padding (the coop ranges: the
+// group waits for its slowest range, which holds the vocabulary's partial last stage)
+template <int G, bool PAIRS, class Tail = NoTail, class Hook = NoHook, bool HALF_LAST = false>
 __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, uint64_t nidx, int wave, int sgn,
                                              int hf, const float (&hB)[64], int s0, int s1, RowState& st,
                                              Stage64Regs& s64, bool preloaded = false, Tail&& tail = Tail(),
@@ -1107,19 +1149,42 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
 #endif
         };
         constexpr int MID = LOGIT_MIDSTORE ? LOGIT_MID_AT : 9;   // 9: never
+        auto mm = [&]() __attribute__((always_inline)) {
+            if constexpr (HALF_LAST) {
+                if (s == s1 - 1 && p.V1 - 64 * s <= 32) {
+                    mfma_stage64_o<MID, true>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
+                    return;
+                }
+            }
+            mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
+        };
         if constexpr (G == 4) {
             if (sgn == MFMA_FIRST_SIGN) {
-                mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
 #if !(DECODE_ABLATE & 1)
-                if constexpr (Hook::replaces) hook(q0, q1, s - 1);
-                else epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
+                if constexpr (Hook::replaces && Hook::early) hook.template part<2>(q0, q1, s - 1);
+#endif
+                mm();
+#if !(DECODE_ABLATE & 1)
+                if constexpr (Hook::replaces) {
+                    if constexpr (Hook::early) hook.template part<5>(q0, q1, s - 1);
+                    else hook(q0, q1, s - 1);
+                } else {
+                    epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
+                }
 #endif
             } else {
 #if !(DECODE_ABLATE & 1)
-                if constexpr (Hook::replaces) hook(q0, q1, s - 1);
-                else epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
+                if constexpr (Hook::replaces) {
+                    if constexpr (Hook::split) hook.template part<1>(q0, q1, s - 1);
+                    else hook(q0, q1, s - 1);
+                } else {
+                    epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
+                }
 #endif
-                mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
+                mm();
+#if !(DECODE_ABLATE & 1)
+                if constexpr (Hook::replaces && Hook::split) hook.template part<6>(q0, q1, s - 1);
+#endif
             }
         } else {
             const float* w1 = wsg + 32 * hf * LDS_ROW;         // this wave's 32-row tile of the stage
@@ -1464,11 +1529,11 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         };
         // SAMPLE: the lane's running max, reference and sum of terms (SampleStage), the logits to the slot
         float sm = -1.0e30f, sref = -1.0e30f;
-        double sT = 0.0, sB = 0.0;
+        double sT = 0.0, sB = 0.0, sP = 0.0;
         if constexpr (SAMPLE) {
             const SampleStage ss{c.slog_r, 16u * (uint32_t)lane_fresh() + SLOG_WAVE_BYTES * (uint32_t)c.wave,
                                  16u * (uint32_t)lane_fresh() + 1024u * (uint32_t)c.wave, (p.V1 + 63) >> 6, sm, sref, sT,
-                                 sB};
+                                 sB, sP};
             logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail, ss);
         } else {
             logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail);
@@ -1504,7 +1569,7 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
             if (p.force_exact)
                 sample_pick<true>(p, c.slog_r, vo, c.hh, mr, lse_s, R, u * T, tok, lp_tok);
             else
-                sample_pick<false>(p, c.slog_r, vo, c.hh, mr, lse_s, R, u * T, tok, lp_tok);
+                sample_pick<false>(p, c.slog_r, vo, c.hh, mr, lse_s, R, u * T, tok, lp_tok, 120 + 24 * (t + 1));
 #endif
         } else {
             const float cv[4] = {st.r0v, st.r1v, __shfl_xor(st.r0v, 32), __shfl_xor(st.r1v, 32)};
@@ -2174,7 +2239,8 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         auto tail = [&]() __attribute__((always_inline)) {
             if (CROSS_PREFETCH && t < p.T) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
         };
-        logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, s0, s1, st, s64, pre && LOGIT_MIDSTORE, tail);
+        logit_stages<4, PAIRS, decltype(tail)&, NoHook, COOP_HALF_LAST>(lds, p, nidx, c.wave, c.sgn, 0, hB, s0, s1, st, s64,
+                                                                        pre && LOGIT_MIDSTORE, tail);
         cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && t < p.T;
         PROF_AT(blockIdx.x, 1024, pm + 1);
         // ---- phase A: this range's partial greedy state, write-through, then the group's merge

@@ -61,6 +61,14 @@ def cell_stages(k, seq):
     print(k, 'median over t=1..15 (us): logit %.1f token %.1f cell %.1f' % tuple(np.median(rows[x]) for x in
                                                                                 ('logit', 'token', 'cell')))
     print(k, 'cell stage m (us):', ' '.join('%d:%.2f' % (m, np.median(v)) for m, v in enumerate(per_m)))
+    if os.environ.get('FITNESS', '') in ('sample', 'self_critical', 'sc_loss'):   # the pick's marks 22, 23
+        sp = {'to_l1': [], 'l1_to_l2': [], 'l2_to_cell': []}
+        for t in range(1, 16):
+            b = 120 + 24 * (t + 1)
+            sp['to_l1'].append(np.median(((ts[:, b + 22] - ts[:, b]) % (1 << 32)) / 100.0))
+            sp['l1_to_l2'].append(np.median(((ts[:, b + 23] - ts[:, b + 22]) % (1 << 32)) / 100.0))
+            sp['l2_to_cell'].append(np.median(((ts[:, b + 1] - ts[:, b + 23]) % (1 << 32)) / 100.0))
+        print(k, 'sampled token phase (us):', ' '.join('%s %.1f' % (n, np.median(v)) for n, v in sp.items()))
 
 
 def split_spans(k, seq, S=4):

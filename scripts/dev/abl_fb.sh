@@ -1,0 +1,6 @@
+set -eo pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/$1; mkdir -p $O
+timeout -k 10 300 python -u scripts/dev/debug_sample_fb.py 512 > $O/fb.log 2>&1
+ABLATE_DIR=ablate_libs FITNESS=${2:-sample} POP=${3:-512} ROUNDS=${4:-3} timeout -k 10 600 python -u scripts/ablate.py > $O/ablate.log 2>&1
+echo ok
