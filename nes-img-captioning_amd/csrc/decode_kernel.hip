@@ -1094,6 +1094,40 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
     else { tok = other; lpv = olp; }
 }
 
+#ifndef LOGIT_FLAGSYNC
+#define LOGIT_FLAGSYNC 0        // 1: the logit loop (G = 4) hands tiles over with per-wave LDS progress words
+#endif
+#define LSYNC_SPIN_TICKS 50000000ull   // 0.5 s of s_memrealtime for a progress wait (then stats[2], and on)
+
+// per-wave progress words of the logit loop (LOGIT_FLAGSYNC): the slowest of the 8 waves
+__device__ __forceinline__ int lsync_min8(const int* a) {
+    int m = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m = min(m, __hip_atomic_load(a + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    return m;
+}
+// wait until every wave's word reached `target` (LDS executes each wave's accesses in order, so the words
+// are set after the accesses they publish; the signal fences keep the compiler from moving LDS accesses across)
+__device__ __forceinline__ void lsync_wait(const int* a, int target, int32_t* stats) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (lsync_min8(a) < target) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (lsync_min8(a) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > LSYNC_SPIN_TICKS) {
+                if (lane_fresh() == 0) atomicAdd(stats + 2, 1);
+                break;
+            }
+        }
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+__device__ __forceinline__ void lsync_set(int* a, int wave, int v) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (lane_fresh() == 0) __hip_atomic_store(a + wave, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 // HALF_LAST: the range's last stage runs chain a only when its rows 32-63 are all padding (the coop ranges: the
 // group waits for its slowest range, which holds the vocabulary's partial last stage)
 template <int G, bool PAIRS, class Tail = NoTail, class Hook = NoHook, bool HALF_LAST = false>
@@ -1124,6 +1158,11 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
     // so the end of a stage has no staging wait and no LDS-write tail in front of the barrier
     if (s0 + 1 < s1) stage64_load_o(lsrc(s0 + 1), lo, bias, s64);
 #endif
+    constexpr bool FS = LOGIT_FLAGSYNC && LOGIT_MIDSTORE && G == 4;
+    __shared__ int lsync[16];                     // FS: [0, 8) tiles written, [8, 16) stages read, per wave
+    if constexpr (FS) {
+        if (threadIdx.x < 16) lsync[threadIdx.x] = 0;
+    }
     __syncthreads();
     f32x16 a0, a1, b0, b1;
 #pragma unroll
@@ -1141,7 +1180,10 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
             // s64 is loaded on every non-last path (at s1 - 2 the load repeats tile s1 - 1): a conditional load
             // here would make the compiler copy the 32 staging registers at every stage to merge the paths
             if (s + 1 < s1) {
+                // FS: the buffer was read in stage s - 1: every wave past it
+                if constexpr (FS) lsync_wait(lsync + 8, s - s0, p.stats);
                 stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
+                if constexpr (FS) lsync_set(lsync, wave, s + 1 - s0);
                 stage64_load_o(lsrc(min(s + 2, s1 - 1)), lo, bias, s64);
             } else {
                 tail();
@@ -1150,13 +1192,18 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
         };
         constexpr int MID = LOGIT_MIDSTORE ? LOGIT_MID_AT : 9;   // 9: never
         auto mm = [&]() __attribute__((always_inline)) {
+            if constexpr (FS) {                      // tile s written by every wave (tile s0: the barrier above)
+                if (s > s0) lsync_wait(lsync, s - s0, p.stats);
+            }
             if constexpr (HALF_LAST) {
                 if (s == s1 - 1 && p.V1 - 64 * s <= 32) {
                     mfma_stage64_o<MID, true>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
+                    if constexpr (FS) lsync_set(lsync + 8, wave, s - s0 + 1);
                     return;
                 }
             }
             mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
+            if constexpr (FS) lsync_set(lsync + 8, wave, s - s0 + 1);
         };
         if constexpr (G == 4) {
             if (sgn == MFMA_FIRST_SIGN) {
@@ -1201,7 +1248,11 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
         stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
 #endif
 #if !(DECODE_ABLATE & 8)
-        __syncthreads();
+        if constexpr (FS) {
+            if (s == s1 - 1) __syncthreads();        // the phase after the loop reuses the buffers
+        } else {
+            __syncthreads();
+        }
 #endif
     };
     auto last = [&](const f32x16& q0, const f32x16& q1, int s) {
@@ -1494,6 +1545,12 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
     const uint64_t nidx = p.noise_idx[c.member];
     // the row's unfinished flag, read now: the token phase needs it right after the logit loop
     const float unf_prev = nl > 0 ? ld1(c.scr_r, lo, U_SLOT) : 0.f;
+    // SAMPLE: the row's uniform for this step, loaded now (the pick's first dependent load otherwise)
+    double u_pre = 0.5;
+    if constexpr (SAMPLE) {
+        if (nl > 0 && c.row_valid)
+            u_pre = p.sample_u[(((size_t)c.member * 2 + c.sgn) * p.B + c.bc) * p.T + (t - 1)];
+    }
     if (t < 0) {
 #pragma unroll
         for (int i = 0; i < 64; ++i) hB[i] = 0.f;               // h = 0 before the first cell
@@ -1552,8 +1609,7 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         float lp_tok = 0.f;                      // seq_logprobs: -lse (the max, greedy) or the draw's log-prob
         bool amb = false;
         if constexpr (SAMPLE) {
-            const size_t ou = (((size_t)c.member * 2 + c.sgn) * p.B + c.bc) * p.T + (t - 1);
-            const double u = c.row_valid ? p.sample_u[ou] : 0.5;
+            const double u = u_pre;
             // the row: max, common reference R, sum T of its terms relative to 2^R (lane 0's part first), lse
             const float mo = __shfl_xor(sm, 32), ro = __shfl_xor(sref, 32);
             const double To = __shfl_xor(sT, 32);

@@ -998,67 +998,18 @@ int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, floa
     hipStream_t s = (hipStream_t)stream;
     HIPC(h, hipSetDevice(h->device));
     const int L = 5, split = 100;                                  // forward_for_sensitivity defaults (nets.py:22)
-    {
-        int rc = ensure_zero_noise(h);
-        if (rc) return rc;
-    }
     if (!h->sens_tok) {
         HIPC(h, hipDeviceSynchronize());
         int rc = dalloc(h, &h->sens_tok, (size_t)2 * h->cfg.max_batch * (L - 1));
         if (rc) return rc;
         h->sens = nicnes_sens_create();
     }
-    // the greedy tokens of logit steps 1..L-1 from the engine's bit-exact decode of theta itself (sigma 0),
-    // every argmax fed back unmasked and no early exit, as forward_for_sensitivity runs (nets.py:48-64)
-    DecodeParams p;
-    p.theta = h->theta32;
-    p.noise = h->zero_noise;
-    p.noise_idx = h->zero_idx;
-    p.fc = h->fc;
-    p.member_batch = nullptr;
-    p.seq = h->sens_tok;
-    p.lp = nullptr;
-    p.scratch = h->dscratch;
-    p.stats = h->stats;
-    p.alive = h->alive;
-    p.alive2 = h->alive + h->alive_stride;
-    p.alive_stride = h->alive_stride;
-    p.part = h->part;
-    p.coop_ctr = h->coop_ctr;
-    p.coop = 0;
-    p.coop_launch = 1;
-    p.test_stall_ms = 0;
-    p.sample_u = nullptr;
-    p.slog = nullptr;
-    p.slog_slots = nullptr;
-    p.slog_ns = 0;
-    p.force_exact = h->force_exact;
-    p.lse_margin = h->lse_margin;
-    p.bounded_lse = 1;
-    p.no_exit = 1;
-    p.no_mask = 1;
-    p.B = rows;
-    p.B_img = h->B;
-    p.rpi = 1;
-    p.sign_off = 0;
-    p.F = h->cfg.fc_feat_size;
-    p.V1 = h->V1;
-    p.T = L - 1;
-    p.D = h->D;
-    // one member: the vocabulary over many workgroups (the split path, two launches per step) instead of one
-    // workgroup walking all 149 logit stages alone (5.9 ms on one CU; r04)
-    const int sns = nslabs_of(rows, 4);
-    p.G = 4;
-    p.S = (int)std::max<int64_t>(1, std::min<int64_t>(32, h->part_cap / sns));
-    p.off_img_w = h->off[0]; p.off_img_b = h->off[1]; p.off_emb_w = h->off[2]; p.off_log_w = h->off[3];
-    p.off_log_b = h->off[4]; p.off_i2h_w = h->off[5]; p.off_i2h_b = h->off[6]; p.off_h2h_w = h->off[7];
-    p.off_h2h_b = h->off[8];
-    HIPC(h, nicnes_launch_decode(&p, 1, sns, s, nullptr, nullptr, nullptr));
     SensParams sp;
     sp.theta = h->theta32;
     sp.fc = h->fc;
-    sp.tok = h->sens_tok;                                          // member 0, sign +: [rows, L - 1]
+    sp.tok = h->sens_tok;                                          // [rows, L - 1], written by the forward
     sp.tok_stride = L - 1;
+    sp.tok_internal = 1;
     sp.Bs = rows;
     sp.V1 = h->V1;
     sp.E = h->cfg.input_encoding_size;

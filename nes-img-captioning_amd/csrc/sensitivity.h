@@ -6,8 +6,9 @@
 struct SensParams {
     const float* theta;          // fp32 theta [D] (flat order)
     const float* fc;             // [Bs, F] unique-image fc rows
-    const int32_t* tok;          // [Bs, tok_stride] greedy tokens of logit steps 1..L-1 (unmasked)
+    int32_t* tok;                // [Bs, tok_stride] greedy tokens of logit steps 1..L-1 (unmasked)
     int32_t tok_stride;
+    int32_t tok_internal;        // 1: the forward picks them itself (argmax of its log_softmax) and writes tok
     int32_t Bs, V1, E, R, F;
     int32_t L;                   // greedy steps (forward_for_sensitivity length = 5)
     int32_t split;               // vocabulary group size (100)

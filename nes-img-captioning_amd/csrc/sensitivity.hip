@@ -19,9 +19,9 @@
 //     the group) - S_k (p Wl): one [Bs, V] x [V, R] product instead of K of them (sens_dh_logit);
 //   * the embedding rows gather dX of the cells whose token is that row: a deterministic per-token sum
 //     (sens_emb_sq), no atomics, so the vector is the same in every process.
-// The greedy tokens of the forward come from the engine's bit-exact decode (unmasked, as
-// forward_for_sensitivity feeds argmax back without the finished mask); the forward activations are
-// recomputed here in fp32. Agreement with the reference's vector is to a stated tolerance (fp32 sums in
+// The forward picks its own greedy tokens (tok_internal: the logits of steps 1..L-1 in the decode's k order, the
+// first id at the log_softmax maximum, fed back unmasked as forward_for_sensitivity does; before r04 a separate
+// split-path decode of theta supplied them, ~1 ms per vector). Agreement with the reference's vector is to a stated tolerance (fp32 sums in
 // another order), not bit for bit.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -240,6 +240,43 @@ __global__ void sens_logsoftmax(const float* Z, float* LP, float* P, int V) {
         lp[v] = l;
         pr[v] = expf(l);
     }
+}
+
+// one block per row: the greedy token of a forward step, torch.max(log_softmax(Z)) (nets.py:61-63): the first id
+// whose log-prob (z - m) - lse equals the maximum, -lse; m, the exp-sum and lse as sens_logsoftmax forms them
+__global__ void sens_greedy(const float* Z, int V, int32_t* tok, int stride, int col) {
+    __shared__ float red[256];
+    __shared__ int redi[256];
+    const float* z = Z + (int64_t)blockIdx.x * V;
+    float m = -INFINITY;
+    for (int v = threadIdx.x; v < V; v += blockDim.x) m = fmaxf(m, z[v]);
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    m = red[0];
+    __syncthreads();
+    float s = 0.f;
+    for (int v = threadIdx.x; v < V; v += blockDim.x) s += expf(z[v] - m);
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    const float lse = logf(red[0]);
+    int best = 0x7fffffff;
+    for (int v = threadIdx.x; v < V; v += blockDim.x)
+        if (((z[v] - m) - lse) == -lse) { best = v; break; }
+    redi[threadIdx.x] = best;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) redi[threadIdx.x] = min(redi[threadIdx.x], redi[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tok[(int64_t)blockIdx.x * stride + col] = redi[0] < V ? redi[0] : 0;
 }
 
 // block (b, k): the seed of output column k for row b through the 2-norm and log_softmax,
@@ -584,6 +621,10 @@ extern "C" int nicnes_sens_run(SensWork* w, const SensParams* p, hipStream_t st)
         hipLaunchKernelGGL(sens_cell_fwd, dim3(blocks((int64_t)Bs * R, 256)), dim3(256), 0, st, Ss(i),
                            i ? (const float*)w->Sh : (const float*)nullptr, bh,
                            i ? (const float*)Cs(i - 1) : (const float*)nullptr, Cs(i), Hs(i), Bs, R);
+        if (p->tok_internal && i >= 1 && i < L) {      // the token fed to cell i + 1 (nets.py:60-63)
+            gemm(sa(Hs(i), 0, R, 1), fwd(targs(Bs, V, R, Wl, 0, 1, R, w->Z, 0, V, 1), bl), 1, st);
+            hipLaunchKernelGGL(sens_greedy, dim3(Bs), dim3(256), 0, st, w->Z, V, p->tok, p->tok_stride, i - 1);
+        }
     }
     gemm(sa(Hs(L), 0, R, 1), fwd(targs(Bs, V, R, Wl, 0, 1, R, w->Z, 0, V, 1), bl), 1, st);             // logit
     hipLaunchKernelGGL(sens_logsoftmax, dim3(Bs), dim3(256), 0, st, w->Z, w->LP, w->P, V);

@@ -333,22 +333,46 @@ extern "C" hipError_t nicnes_launch_noise_vectors(const float* noise, const uint
 // (mode 1: SM-G-SUM, SM-G-ABS, SM-VECTOR divide the noise by the sensitivity) or fp32(fp32(sigma * z) *
 // vec) (mode 2: SM-PROPORTIONAL multiplies it by |theta|), IEEE division as torch's in-place /=.
 // out row k at out + k * out_stride.
+__device__ __forceinline__ float mutate1(float z, float sigma, float v, int mode) {
+    const float d = sigma * z;
+    return mode == 1 ? d / v : d * v;
+}
+
+// VEC: 4 consecutive parameters per thread and one 16-byte store (the member's table slice starts at any float:
+// its loads stay dword-aligned 16-byte loads); the same per-element arithmetic as the scalar form
+template <bool VEC>
 __global__ __launch_bounds__(256) void nicnes_mutate_kernel(const float* noise, const uint64_t* idx, int64_t dim,
                                                             float sigma, const float* vec, int mode, float* out,
                                                             int64_t out_stride) {
     const int k = blockIdx.y;
     const float* z = noise + idx[k];
     float* o = out + (size_t)k * out_stride;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < dim; j += (int64_t)gridDim.x * blockDim.x) {
-        const float d = sigma * z[j];
-        o[j] = mode == 1 ? d / vec[j] : d * vec[j];
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    int64_t j0 = 0;
+    if constexpr (VEC) {
+        const int64_t n4 = dim / 4;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += step) {
+            f32x4 zv, r;
+            __builtin_memcpy(&zv, z + 4 * i, 16);
+            const f32x4 vv = reinterpret_cast<const f32x4*>(vec)[i];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) r[e] = mutate1(zv[e], sigma, vv[e], mode);
+            reinterpret_cast<f32x4*>(o)[i] = r;
+        }
+        j0 = 4 * n4;
     }
+    for (int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < dim; j += step)
+        o[j] = mutate1(z[j], sigma, vec[j], mode);
 }
 
 extern "C" hipError_t nicnes_launch_mutate(const float* noise, const uint64_t* idx, int count, int64_t dim, float sigma,
                                            const float* vec, int mode, float* out, int64_t out_stride, hipStream_t s) {
-    hipLaunchKernelGGL(nicnes_mutate_kernel, dim3(512, count), dim3(256), 0, s, noise, idx, dim, sigma, vec, mode, out,
-                       out_stride);
+    if (out_stride % 4 == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)vec & 15) == 0)
+        hipLaunchKernelGGL(nicnes_mutate_kernel<true>, dim3(512, count), dim3(256), 0, s, noise, idx, dim, sigma, vec,
+                           mode, out, out_stride);
+    else
+        hipLaunchKernelGGL(nicnes_mutate_kernel<false>, dim3(512, count), dim3(256), 0, s, noise, idx, dim, sigma, vec,
+                           mode, out, out_stride);
     return hipGetLastError();
 }
 
