@@ -320,10 +320,11 @@ def main():
         step_ms = float(np.mean([q['step_ms'] for q in phases]))
         flops = decode_flops_per_member(rows) * P_local
         step_flop = step_flops_per_member(rows) * P_local
-        # per workgroup and logit step: every 64-row stage's logits (64 KiB) and its lanes' stage sums (8 KiB)
+        # per workgroup and logit step: every 64-row stage's logits (64 KiB), its lanes' stage sums (8 KiB) and 8 KiB per 8 stages
         # written to the slot; the pick's reads (the stage sums up to the crossing stage, then one stage's
         # logits per row) are not counted
-        slog_bytes = 16 * nslabs * ((9488 + 63) // 64) * 73728
+        nst = (9488 + 63) // 64
+        slog_bytes = 16 * nslabs * (nst * 73728 + (nst + 7) // 8 * 8192)   # + the 8-stage block records
         alg_bytes = (step_noise_bytes_per_member(rows) + slog_bytes) * P_local
     elif not ph['step_launches'] and not ph['logit_launches']:
         # two-stream decode (NICNES_DECODE_STREAMS=2): the halves' launches overlap, so the whole decode

@@ -763,6 +763,9 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
 #define COOP_HALF_LAST 0         // 1: coop ranges run a last stage of padding rows 32-63 as chain a only (spills
                                  // 12 VGPRs inside the stage loop at the 256-VGPR budget: not adopted)
 #endif
+#ifndef SLOG_LOGIT_POLICY
+#define SLOG_LOGIT_POLICY SLOG_STORE_POLICY   // the logit words' own policy (the {P, r} and block records: the above)
+#endif
 #ifndef SAMP_SPLIT_STORES
 #define SAMP_SPLIT_STORES 0      // 1: the late sign's stores after its MFMAs (+2.5 % sampled kernel time, measured)
 #endif
@@ -835,8 +838,8 @@ struct SampleStage {
             for (int k = 0; k < 4; ++k) {
                 const f32x4 a = {q0[4 * k], q0[4 * k + 1], q0[4 * k + 2], q0[4 * k + 3]};
                 const f32x4 b = {q1[4 * k], q1[4 * k + 1], q1[4 * k + 2], q1[4 * k + 3]};
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), slot, (int)vo, (int)(so + 1024u * k), SLOG_STORE_POLICY);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), slot, (int)vo, (int)(so + 1024u * (4 + k)), SLOG_STORE_POLICY);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), slot, (int)vo, (int)(so + 1024u * k), SLOG_LOGIT_POLICY);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), slot, (int)vo, (int)(so + 1024u * (4 + k)), SLOG_LOGIT_POLICY);
             }
         }
 #endif
