@@ -88,7 +88,8 @@ PRESETS = {
 # committed PMC profiles: profiles/<round>_pmc_<key>_p<members per GPU>_b<B>.json
 PMC_KEYS = {'nicnes_decode_steps_kernel': 'steps', 'nicnes_decode_step_kernel': 'step',
             'nicnes_decode_logit_kernel<4>': 'logit', 'nicnes_decode_coop_kernel<4>': 'coop4',
-            'nicnes_decode_coop_kernel<2>': 'coop2', 'nicnes_decode_steps2_kernel': 'steps2'}
+            'nicnes_decode_coop_kernel<2>': 'coop2', 'nicnes_decode_steps2_kernel': 'steps2',
+            'nicnes_decode_steps_kernel<sample>': 'sampled'}
 KERNEL_SOURCES = ('nes-img-captioning_amd/csrc/decode_kernel.hip', 'nes-img-captioning_amd/csrc/decode_kernel.h',
                   'include/nicnes_math.h')
 
