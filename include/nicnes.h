@@ -175,9 +175,12 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
  * antithetic signs are theta, so sign + decodes the first ceil(B/2) images and sign - the rest and
  * the halves are scored as one rollout: seq_out [B, seq_length] int32 and logprob_out [B, seq_length]
  * (both nullable, rows 0..B-1 in batch order) and the fitness equal nicnes_evaluate_lp's sign-+
- * row of a sigma = 0 member bit for bit, at half its decode work. */
-int nicnes_evaluate_theta(nicnes_handle* h, int32_t batch, double* fitness_out, int32_t* seq_out, float* logprob_out,
-                          void* stream);
+ * row of a sigma = 0 member bit for bit, at half its decode work. The sampled fitness modes draw from
+ * the stream of `iteration` reserved for eval rollouts (member index 2^32 - 1 in the draw hash), so each
+ * eval rollout draws afresh, as the reference's worker RNG does, and never shares an evolve member's
+ * draws. */
+int nicnes_evaluate_theta(nicnes_handle* h, int32_t batch, uint64_t iteration, double* fitness_out, int32_t* seq_out,
+                          float* logprob_out, void* stream);
 
 /* Centred ranks + antithetic weights over the WHOLE population, replaces
  * NESMaster.compute_centered_ranks and the weights line of gradient_estimate

@@ -858,7 +858,9 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
                 return fail(h, NICNES_ERR_INVALID, "nicnes_set_sample_draws: count x 2 x B x seq_length draws needed");
             HIPC(h, hipMemcpyAsync(h->su, h->su_host.data(), (size_t)need * sizeof(double), hipMemcpyHostToDevice, s));
         } else {
-            HIPC(h, nicnes_launch_sample_draws(h->cfg.noise_seed, iteration, (uint64_t)member_begin, count, rows,
+            // eval rollouts (eval_theta) draw from a member index no population reaches
+            HIPC(h, nicnes_launch_sample_draws(h->cfg.noise_seed, iteration,
+                                               eval_theta ? (uint64_t)0xffffffffu : (uint64_t)member_begin, count, rows,
                                                h->cfg.seq_length, h->su, s));
         }
         p.sample_u = h->su;
@@ -981,13 +983,13 @@ int nicnes_evaluate_batches(nicnes_handle* h, uint64_t iteration, int32_t member
                          stream, false);
 }
 
-int nicnes_evaluate_theta(nicnes_handle* h, int32_t batch, double* fitness_out, int32_t* seq_out, float* logprob_out,
-                          void* stream) {
+int nicnes_evaluate_theta(nicnes_handle* h, int32_t batch, uint64_t iteration, double* fitness_out, int32_t* seq_out,
+                          float* logprob_out, void* stream) {
     if (!h) return NICNES_ERR_INVALID;
     if (batch < 0 || (h->batch_set && batch >= h->n_batches)) return fail(h, NICNES_ERR_INVALID, "batch outside [0, n_batches)");
     const int32_t mb = batch;
-    return evaluate_impl(h, 0, 0, 1, 0.f, h->n_batches > 1 ? &mb : nullptr, fitness_out, seq_out, logprob_out, stream,
-                         true);
+    return evaluate_impl(h, iteration, 0, 1, 0.f, h->n_batches > 1 ? &mb : nullptr, fitness_out, seq_out, logprob_out,
+                         stream, true);
 }
 
 int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, float* out, void* stream) {

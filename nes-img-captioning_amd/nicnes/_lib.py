@@ -71,7 +71,7 @@ def lib(path=None):
         'nicnes_set_batches': (c.c_int, [vp, vp, i32, i32, vp, i32, vp, vp]),
         'nicnes_set_mutation': (c.c_int, [vp, i32, vp, vp]),
         'nicnes_evaluate_batches': (c.c_int, [vp, u64, i32, i32, f32, vp, vp, vp, vp, vp]),
-        'nicnes_evaluate_theta': (c.c_int, [vp, i32, vp, vp, vp, vp]),
+        'nicnes_evaluate_theta': (c.c_int, [vp, i32, u64, vp, vp, vp, vp]),
         'nicnes_set_sample_draws': (c.c_int, [vp, vp, i64]),
         'nicnes_set_rows_per_image': (c.c_int, [vp, i32]),
         'nicnes_rank_weights': (c.c_int, [vp, vp, i32, vp, vp, vp]),

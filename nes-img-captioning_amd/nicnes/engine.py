@@ -256,16 +256,18 @@ class Engine:
               'set_sample_draws')
         self._keep['draws'] = a
 
-    def evaluate_theta(self, batch=0, return_seq=False, return_lp=False):
+    def evaluate_theta(self, batch=0, return_seq=False, return_lp=False, iteration=0):
         """Fitness of theta itself on the batch held (or batch `batch` of set_batches'): the sigma = 0
         rollout (CaptPolicy.rollout) decoded once, sign + over the first half of the images and sign -
-        over the rest. Tensor [1] fp64 on the GPU; return_seq / return_lp add [B, T] tokens / log-probs."""
+        over the rest. Tensor [1] fp64 on the GPU; return_seq / return_lp add [B, T] tokens / log-probs.
+        iteration: the draw stream of the sampled modes (each eval rollout its own)."""
         fit = torch.empty(1, dtype=torch.float64, device=self.device)
         shape = (self.rollout_rows(), self.cfg.seq_length)
         seq = torch.empty(shape, dtype=torch.int32, device=self.device) if return_seq else None
         lp = torch.empty(shape, dtype=torch.float32, device=self.device) if return_lp else None
         with torch.cuda.device(self.device):
-            check(self.L.nicnes_evaluate_theta(self.h, int(batch), _ptr(fit), _ptr(seq), _ptr(lp), self._stream()),
+            check(self.L.nicnes_evaluate_theta(self.h, int(batch), int(iteration), _ptr(fit), _ptr(seq), _ptr(lp),
+                                               self._stream()),
                   self.h, 'evaluate_theta')
         out = (fit,) + ((seq,) if return_seq else ()) + ((lp,) if return_lp else ())
         return out if len(out) > 1 else fit

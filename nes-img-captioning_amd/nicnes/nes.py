@@ -185,7 +185,9 @@ class EnginePolicy:
         self._ensure_batch(data)
         # theta itself, decoded once (nicnes_evaluate_theta: the two antithetic signs split the images);
         # with several batches held, member 0's batch (member_batches' rule)
-        fit = self.e.evaluate_theta(0)
+        # the sampled modes draw afresh per eval rollout, as the reference's worker RNG does
+        self._eval_calls = getattr(self, '_eval_calls', 0) + 1
+        fit = self.e.evaluate_theta(0, iteration=self._eval_calls)
         return float(fit[0].item())
 
 

@@ -103,7 +103,7 @@ class OracleEngine:
                 out[k, s] = CR.criterion_fitness(self.fitness_mode, lp, seq, scores) if self.fitness_mode else f
         return out
 
-    def evaluate_theta(self, batch=0):
+    def evaluate_theta(self, batch=0, iteration=0):
         fc, gts = (self.fc, self.gts) if not getattr(self, 'batches', None) else self.batches[batch]
         seq, lp, _ = O.decode(self.dims, self.theta32, fc)
         f, scores = CR.rollout_fitness(self.scorer, seq, gts)

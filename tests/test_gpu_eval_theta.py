@@ -101,3 +101,23 @@ def test_eval_theta_on_a_named_batch(eng):
         assert f1[0] == f2[0, 0], (b, f1, f2)
     with pytest.raises(Exception):
         eng.evaluate_theta(3)
+
+
+def test_eval_theta_sampled_draws_follow_the_iteration(eng):
+    """Sampled modes: an eval rollout draws from its own stream per iteration, reproducibly, and not
+    from an evolve member's (the sigma = 0 member 0 of the same iteration decodes other captions)."""
+    dims = O.Dims()
+    theta = O.make_theta(dims, 2, 4.0, 0.1)
+    fc, gts, df, n = _batch(dims, theta, 40, 7)
+    _load(eng, theta, [(fc, gts)], df, n)
+    try:
+        eng.set_fitness_mode('sample')
+        _, s1 = eng.evaluate_theta(0, return_seq=True, iteration=1)
+        _, s1b = eng.evaluate_theta(0, return_seq=True, iteration=1)
+        _, s2 = eng.evaluate_theta(0, return_seq=True, iteration=2)
+        _, sm = eng.evaluate(1, 0, 1, 0.0, return_seq=True)
+        assert torch.equal(s1, s1b)
+        assert not torch.equal(s1, s2)
+        assert not torch.equal(s1, sm[0, 0])
+    finally:
+        eng.set_fitness_mode('greedy')

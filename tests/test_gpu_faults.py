@@ -159,7 +159,7 @@ def test_eval_theta_writes_exactly_its_rows(B):
         lp = torch.full((B + 2, T), -7.0, dtype=torch.float32, device=e.device)
         fit = torch.empty(1, dtype=torch.float64, device=e.device)
         with torch.cuda.device(e.device):
-            _lib.check(e.L.nicnes_evaluate_theta(e.h, 0, ctypes.c_void_p(fit.data_ptr()),
+            _lib.check(e.L.nicnes_evaluate_theta(e.h, 0, 0, ctypes.c_void_p(fit.data_ptr()),
                                                  ctypes.c_void_p(seq.data_ptr()), ctypes.c_void_p(lp.data_ptr()),
                                                  e._stream()), e.h, 'evaluate_theta')
         torch.cuda.synchronize()
