@@ -27,6 +27,7 @@
 // compiler would otherwise spill them and reload them behind in-flight staging loads.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "../../include/nicnes_math.h"
 #include "decode_kernel.h"
@@ -760,8 +761,8 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
 #define SLOG_BLOCK 8
 #define SLOG_BLK_BYTES 8192u
 #ifndef COOP_HALF_LAST
-#define COOP_HALF_LAST 0         // 1: coop ranges run a last stage of padding rows 32-63 as chain a only (spills
-                                 // 12 VGPRs inside the stage loop at the 256-VGPR budget: not adopted)
+#define COOP_HALF_LAST 0         // 1: coop ranges run a last stage of padding rows 32-63 as chain a only, after
+                                 // the stage loop (measured +1.3 % at P = 64, +2.2 % at P = 128: not adopted)
 #endif
 #ifndef SLOG_LOGIT_POLICY
 #define SLOG_LOGIT_POLICY SLOG_STORE_POLICY   // the logit words' own policy (the {P, r} and block records: the above)
@@ -1170,7 +1171,8 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
     f32x16 a0, a1, b0, b1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { b0[r] = NEG_INF; b1[r] = NEG_INF; }
-    auto stage = [&](int s, f32x16& o0, f32x16& o1, const f32x16& q0, const f32x16& q1) {
+    auto stage = [&](auto halfc, int s, f32x16& o0, f32x16& o1, const f32x16& q0, const f32x16& q1) {
+        constexpr bool HS = decltype(halfc)::value;    // HALF_LAST: this is the range's partial last stage
         const int sn = min(s + 1, s1 - 1);
 #if !LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
         stage64_load_o(lsrc(sn), lo, bias, s64);
@@ -1198,14 +1200,7 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
             if constexpr (FS) {                      // tile s written by every wave (tile s0: the barrier above)
                 if (s > s0) lsync_wait(lsync, s - s0, p.stats);
             }
-            if constexpr (HALF_LAST) {
-                if (s == s1 - 1 && p.V1 - 64 * s <= 32) {
-                    mfma_stage64_o<MID, true>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
-                    if constexpr (FS) lsync_set(lsync + 8, wave, s - s0 + 1);
-                    return;
-                }
-            }
-            mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
+            mfma_stage64_o<MID, HS>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
             if constexpr (FS) lsync_set(lsync + 8, wave, s - s0 + 1);
         };
         if constexpr (G == 4) {
@@ -1266,15 +1261,44 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
             epilogue32<PAIRS>(st, q0, 64 * s + vl);
         }
     };
-    for (int s = s0; s < s1; s += 2) {
-        stage(s, a0, a1, b0, b1);
-        if (s + 1 == s1) {
-            last(a0, a1, s);
+    using F_ = std::false_type;
+    if constexpr (!HALF_LAST) {
+        for (int s = s0; s < s1; s += 2) {
+            stage(F_{}, s, a0, a1, b0, b1);
+            if (s + 1 == s1) {
+                last(a0, a1, s);
+                return;
+            }
+            stage(F_{}, s + 1, b0, b1, a0, a1);
+        }
+        last(b0, b1, s1 - 1);
+    } else {
+        // the partial last stage (rows 32-63 all padding) after the loop, as its own instantiation: inside the
+        // loop body its second MFMA form made the loop spill
+        const bool half = p.V1 - 64 * (s1 - 1) <= 32 && s1 - s0 >= 2;
+        const int se = half ? s1 - 1 : s1;
+        bool odd = false;
+        for (int s = s0; s < se; s += 2) {
+            stage(F_{}, s, a0, a1, b0, b1);
+            if (s + 1 == se) {
+                odd = true;
+                break;
+            }
+            stage(F_{}, s + 1, b0, b1, a0, a1);
+        }
+        if (!half) {
+            if (odd) last(a0, a1, se - 1);
+            else last(b0, b1, se - 1);
             return;
         }
-        stage(s + 1, b0, b1, a0, a1);
+        if (odd) {
+            stage(std::true_type{}, se, b0, b1, a0, a1);
+            last(b0, b1, se);
+        } else {
+            stage(std::true_type{}, se, a0, a1, b0, b1);
+            last(a0, a1, se);
+        }
     }
-    last(b0, b1, s1 - 1);
 }
 
 // gate tiles of the cell: tile m = 0..19 is gate chunk tile_q(m) (order g1, g2, i, f, o) of the
