@@ -333,7 +333,15 @@ __global__ __launch_bounds__(64) void nicnes_img_ngram_kernel(const int32_t* img
 // Rows per workgroup: 32, or 8 when there are few candidates (64 members per GPU: 128 candidates), so that the
 // launch still has >= ~2048 workgroups to hide the probe latency (the P = 64 rollouts: DESIGN §5).
 #define CIDER_IMG_ROWS 32
-__global__ __launch_bounds__(256) void nicnes_cider_img_kernel(const int32_t* seq, int B, int T, CiderTables tb,
+#ifndef CIDER_WPE
+#define CIDER_WPE 0                // > 0: amdgpu_waves_per_eu bound of the image kernel (register budget)
+#endif
+#if CIDER_WPE
+#define CIDER_IMG_ATTR __attribute__((amdgpu_waves_per_eu(CIDER_WPE)))
+#else
+#define CIDER_IMG_ATTR
+#endif
+__global__ __launch_bounds__(256) CIDER_IMG_ATTR void nicnes_cider_img_kernel(const int32_t* seq, int B, int T, CiderTables tb,
                                                                const int32_t* img_ref_start, const int32_t* member_batch,
                                                                double* scores, int rpi, int rows_wg) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
