@@ -653,12 +653,6 @@ extern "C" int nicnes_sens_run(SensWork* w, const SensParams* p, hipStream_t st)
     }
     hipLaunchKernelGGL(sens_dh_logit, dim3(Bs, K), dim3(R), 0, st, w->LP, w->IG, w->SG, w->PW, Wl, w->dH, Bs, V, K, R,
                        p->split);
-    static const int dump = getenv("NICNES_SENS_DUMP") ? atoi(getenv("NICNES_SENS_DUMP")) : 0;   // dev: intermediates
-    if (dump == 1) return hipMemcpyAsync(p->out, w->dH, (size_t)K * Bs * R * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
-    if (dump == 6) return hipMemcpyAsync(p->out, w->LP, (size_t)Bs * V * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
-    if (dump == 7) return hipMemcpyAsync(p->out, w->IG, (size_t)Bs * K * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
-    if (dump == 8) return hipMemcpyAsync(p->out, w->SG, (size_t)Bs * K * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
-    if (dump == 4) return hipMemcpyAsync(p->out, w->PW, (size_t)Bs * R * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
     if (hipMemsetAsync(w->dC, 0, (size_t)K * Bs * R * sizeof(float), st) != hipSuccess) return 4;
     const int64_t sdk = L1 * Bs * G5, sxk = L1 * Bs * E;
     for (int i = L; i >= 0; --i) {
@@ -669,22 +663,6 @@ extern "C" int nicnes_sens_run(SensWork* w, const SensParams* p, hipStream_t st)
         gemm(sa(dSi, sdk, G5, 1), targs(Bs, E, G5, Wi, 0, E, 1, w->dX + (int64_t)i * Bs * E, sxk, E, 1), K, st);
         if (i >= 1)
             gemm(sa(dSi, sdk, G5, 1), targs(Bs, R, G5, Wh, 0, R, 1, w->dH, (int64_t)Bs * R, R, 1), K, st);
-        static const int dcell = getenv("NICNES_SENS_CELL") ? atoi(getenv("NICNES_SENS_CELL")) : L;
-        if (dump == 2 && i == dcell) {   // dS of cell dcell, [K][Bs][5R] (strided rows copied one k at a time)
-            for (int k = 0; k < K; ++k)
-                if (hipMemcpyAsync(p->out + (int64_t)k * Bs * G5, dSi + k * sdk, (size_t)Bs * G5 * sizeof(float),
-                                   hipMemcpyDeviceToDevice, st)) return 7;
-            return 0;
-        }
-        if (dump == 3 && i == dcell) {   // dX of cell dcell, [K][Bs][E]
-            for (int k = 0; k < K; ++k)
-                if (hipMemcpyAsync(p->out + (int64_t)k * Bs * E, w->dX + (int64_t)i * Bs * E + k * sxk, (size_t)Bs * E * sizeof(float),
-                                   hipMemcpyDeviceToDevice, st)) return 7;
-            return 0;
-        }
-        if (dump == 5 && i == dcell) {   // dH fed to cell dcell - 1, [K][Bs][R]
-            return hipMemcpyAsync(p->out, w->dH, (size_t)K * Bs * R * sizeof(float), hipMemcpyDeviceToDevice, st) ? 7 : 0;
-        }
     }
     // gate weights: G_k[g, e] = sum over (cell i, b) of dS_k[i, b, g] X_i[b, e] (h2h: cells 1..L with H_{i-1})
     sqsum(sa(w->dS, sdk, 1, G5), targs(G5, E, (int)(L1 * Bs), w->X, 0, E, 1, part + p->off_i2h_w, D, E, 1), K, SENS_NZ, st);
