@@ -489,3 +489,21 @@ def test_mutation_worker_with_state_dict_models(workload):
     for tid in (1, 2):
         res = w.fitness_batch(tid, N.NESTask(current=sd, batch_data=batch, noise_stdev=0.05, iteration=tid), 0, 2)
         assert len(res) == 2 and e.mutation[0] == 'scale'
+
+
+def test_eval_rollouts_draw_a_fresh_stream_each(workload):
+    """EnginePolicy.rollout (the eval result, CaptPolicy.rollout) hands nicnes_evaluate_theta a new draw iteration
+    per call, as the reference worker's RNG draws afresh per eval (not iteration 0 every time)."""
+    e = _engine(workload)
+    seen = []
+    orig = e.evaluate_theta
+
+    def spy(batch=0, iteration=0, **kw):
+        seen.append(iteration)
+        return orig(batch, iteration=iteration)
+    e.evaluate_theta = spy
+    pol = N.EnginePolicy(e)
+    data = {'fc_feats': np.repeat(workload[2], 5, axis=0), 'gts': workload[3]}
+    pol.rollout(None, data, None)
+    pol.rollout(None, data, None)
+    assert seen == [1, 2]
