@@ -27,7 +27,6 @@
 // compiler would otherwise spill them and reload them behind in-flight staging loads.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <type_traits>
 
 #include "../../include/nicnes_math.h"
 #include "decode_kernel.h"
@@ -381,9 +380,7 @@ struct NoMid {
 
 // mid() runs before half-chunk MID of the 8 (8: after the last MFMA; 9: never): the logit loop's W+- store
 // of the next stage and the loads of the one after (LOGIT_MIDSTORE)
-// HALF: chain a only (a stage whose rows 32-63 are all padding: acc1 keeps the padding bias, -inf, which is
-// what the skipped products would leave in it)
-template <int MID = 8, bool HALF = false, class Mid = NoMid>
+template <int MID = 8, class Mid = NoMid>
 __device__ __forceinline__ void mfma_stage64_o(const float* w, const float* bias, const float (&Bop)[64], int arow,
                                                int hh, f32x16& acc0, f32x16& acc1, Mid&& mid = Mid()) {
     const float* row0 = w + arow;
@@ -404,14 +401,13 @@ __device__ __forceinline__ void mfma_stage64_o(const float* w, const float* bias
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             a0[c] = *reinterpret_cast<const f32x4*>(row0 + T * 32 + 4 * c);
-            if constexpr (!HALF) a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
+            a1[c] = *reinterpret_cast<const f32x4*>(row1 + T * 32 + 4 * c);
         }
 #pragma unroll
         for (int jj = 0; jj < 16; ++jj) {
             if (jj == 8) at(2 * T + 1);
             acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[jj >> 2][jj & 3], Bop[16 * T + jj], acc0, 0, 0, 0);
-            if constexpr (!HALF)
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[jj >> 2][jj & 3], Bop[16 * T + jj], acc1, 0, 0, 0);
         }
     }
     at(8);
@@ -760,19 +756,6 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
 // loads and then the crossing stage in one
 #define SLOG_BLOCK 8
 #define SLOG_BLK_BYTES 8192u
-#ifndef COOP_HALF_LAST
-#define COOP_HALF_LAST 0         // 1: coop ranges run a last stage of padding rows 32-63 as chain a only, after
-                                 // the stage loop (measured +1.3 % at P = 64, +2.2 % at P = 128: not adopted)
-#endif
-#ifndef SLOG_LOGIT_POLICY
-#define SLOG_LOGIT_POLICY SLOG_STORE_POLICY   // the logit words' own policy (the {P, r} and block records: the above)
-#endif
-#ifndef SAMP_SPLIT_STORES
-#define SAMP_SPLIT_STORES 0      // 1: the late sign's stores after its MFMAs (+2.5 % sampled kernel time, measured)
-#endif
-#ifndef SAMP_EARLY_STORES
-#define SAMP_EARLY_STORES 0      // 1: the early sign's logit stores before its MFMAs
-#endif
 #ifndef SAMP_L1_ROUND
 #define SAMP_L1_ROUND 20         // block records per round of the pick's level 1 (V1 <= 10240: one round)
 #endif
@@ -800,21 +783,15 @@ __device__ __forceinline__ double samp_scale(double x, float e) {
 // place of the greedy epilogue
 struct NoHook {
     static constexpr bool replaces = false;
-    static constexpr bool split = false;
-    static constexpr bool early = false;
     __device__ __forceinline__ void operator()(const f32x16&, const f32x16&, int) const {}
-    template <int MODE>
-    __device__ __forceinline__ void part(const f32x16&, const f32x16&, int) const {}
 };
 
 // the sampled decode's logit loop epilogue: running max m, reference r = ceil(m log2e), the lane's running sum T
 // of its terms relative to 2^r; stores the stage's logits and {P, r} to the slot (one wave instruction per
-// 1 KiB word). part<1> is the arithmetic, part<2> the stores (`split`: the waves whose epilogue runs before
-// their MFMAs issue the stores after them, behind that stage's staging loads)
+// 1 KiB word; non-temporal). Measured and not kept (git history, r04): the late sign's stores after its MFMAs
+// (+2.5 %), the early sign's logit stores before them (+0.7 %), sc1 / sc0 sc1 / sc1 nt logit stores (+1-2 %).
 struct SampleStage {
     static constexpr bool replaces = true;
-    static constexpr bool split = SAMP_SPLIT_STORES;
-    static constexpr bool early = SAMP_EARLY_STORES;
     rsrc_t slot;
     uint32_t vo;      // 16 * lane + SLOG_WAVE_BYTES * wave
     uint32_t vb;      // 16 * lane + 1024 * wave (block records)
@@ -823,54 +800,42 @@ struct SampleStage {
     float& ref;
     double& T;
     double& Bk;       // the current block's sum of terms relative to 2^ref
-    double& Pp;       // the stage's own sum (part<1> -> part<2>)
     __device__ __forceinline__ void operator()(const f32x16& q0, const f32x16& q1, int s) const {
-        part<7>(q0, q1, s);
-    }
-    // MODE bit 1: the arithmetic; bit 2: the logit stores; bit 4: the {P, r} and block records
-    template <int MODE>
-    __device__ __forceinline__ void part(const f32x16& q0, const f32x16& q1, int s) const {
         if (s < 0) return;                               // the pipeline's first epilogue: no stage yet
         const uint32_t so = SLOG_STAGE_BYTES * (uint32_t)s;
-        constexpr bool ARITH = (MODE & 1) != 0, STORES = (MODE & 2) != 0, RECS = (MODE & 4) != 0;
 #if !(DECODE_ABLATE & 256)
-        if constexpr (STORES) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const f32x4 a = {q0[4 * k], q0[4 * k + 1], q0[4 * k + 2], q0[4 * k + 3]};
-                const f32x4 b = {q1[4 * k], q1[4 * k + 1], q1[4 * k + 2], q1[4 * k + 3]};
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), slot, (int)vo, (int)(so + 1024u * k), SLOG_LOGIT_POLICY);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), slot, (int)vo, (int)(so + 1024u * (4 + k)), SLOG_LOGIT_POLICY);
-            }
+        for (int k = 0; k < 4; ++k) {
+            const f32x4 a = {q0[4 * k], q0[4 * k + 1], q0[4 * k + 2], q0[4 * k + 3]};
+            const f32x4 b = {q1[4 * k], q1[4 * k + 1], q1[4 * k + 2], q1[4 * k + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), slot, (int)vo, (int)(so + 1024u * k), SLOG_STORE_POLICY);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), slot, (int)vo, (int)(so + 1024u * (4 + k)), SLOG_STORE_POLICY);
         }
 #endif
-        if constexpr (ARITH) {
-            const float mnew = vmax2(m, vmax2(vmax16(q0), vmax16(q1)));
-            const float rnew = ceilf(mnew * LOG2E);
-            if (rnew > ref) {
-                T = samp_scale(T, ref - rnew);
-                Bk = samp_scale(Bk, ref - rnew);
-                ref = rnew;
-            }
-            m = mnew;
-            double P = 0.0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                float qa[4], qb[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    qa[e] = samp_p(q0[4 * k + e], ref);
-                    qb[e] = samp_p(q1[4 * k + e], ref);
-                }
-                P += (double)samp_group(qa);
-                P += (double)samp_group(qb);
-            }
-            T += P;
-            Bk += P;
-            Pp = P;
+        const float mnew = vmax2(m, vmax2(vmax16(q0), vmax16(q1)));
+        const float rnew = ceilf(mnew * LOG2E);
+        if (rnew > ref) {
+            T = samp_scale(T, ref - rnew);
+            Bk = samp_scale(Bk, ref - rnew);
+            ref = rnew;
         }
-        if constexpr (RECS) {
-            const uint64_t pb = __builtin_bit_cast(uint64_t, Pp);
+        m = mnew;
+        double P = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float qa[4], qb[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                qa[e] = samp_p(q0[4 * k + e], ref);
+                qb[e] = samp_p(q1[4 * k + e], ref);
+            }
+            P += (double)samp_group(qa);
+            P += (double)samp_group(qb);
+        }
+        T += P;
+        Bk += P;
+        {
+            const uint64_t pb = __builtin_bit_cast(uint64_t, P);
             const u32x4 w = {(uint32_t)pb, (uint32_t)(pb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
             __builtin_amdgcn_raw_buffer_store_b128(w, slot, (int)vo, (int)(so + 8u * 1024u), SLOG_STORE_POLICY);
             asm volatile("s_nop 1" ::"v"(w));                // (the wait states of the block record below)
@@ -972,9 +937,6 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
         const uint32_t vb = 16u * (uint32_t)(threadIdx.x & 63) + 1024u * (uint32_t)(threadIdx.x >> 6);
         int qf = -1;
         double cq = 0.0, cl = 0.0;
-#ifdef SAMPLE_BLOCK_CHECK
-        double sblk = 0.0;
-#endif
         for (int q0 = 0; q0 < nblk; q0 += SAMP_L1_ROUND) {
             // B and r as their own loads (a 16-byte load narrowed by the compiler returned B's low word as r)
             double Bw[SAMP_L1_ROUND];
@@ -991,29 +953,9 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
                     const double a = samp_scale(Bw[j], rw[j] - R);
                     const double ao = __shfl_xor(a, 32);
                     const double S = hh == 0 ? a + ao : ao + a;
-#ifdef SAMPLE_BLOCK_CHECK
-                    {
-                        const int q = q0 + j, qa = SLOG_BLOCK * q, qn = min(SLOG_BLOCK, nst - qa);
-                        double tot = 0.0;
-                        for (int i = 0; i < qn; ++i) {
-                            const uint32_t o = vo + SLOG_STAGE_BYTES * (uint32_t)(qa + i) + 8u * 1024u;
-                            const double P = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(lr, (int)o, 0, 16));
-                            const float r = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (int)o + 8, 0, 16));
-                            tot += samp_scale(P, r - R);
-                        }
-                        const double a0 = samp_scale(Bw[j], rw[j] - R);
-                        if (fabs(tot - a0) > 1e-9 * fabs(tot))
-                            printf("BLKCHK blk %d nblk %d lane %d wave %d qf %d Sblk %.17g stages %.17g r %g R %g\n", q, nblk,
-                                   (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), qf, a0, tot, rw[j], R);
-                    }
-#endif
                     if (qf < 0) {
-                        if (cum + S > thr) {
-                            qf = q0 + j; cq = cum;
-#ifdef SAMPLE_BLOCK_CHECK
-                            sblk = S;
-#endif
-                        } else { cl = cum; cum += S; }
+                        if (cum + S > thr) { qf = q0 + j; cq = cum; }
+                        else { cl = cum; cum += S; }
                     }
                 }
             }
@@ -1045,17 +987,6 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
             }
         }
         if (!have) { sf = sa + sn - 1; cb = csl; rf = rl; }     // the block's stage sums stop short: its last stage
-#ifdef SAMPLE_BLOCK_CHECK
-        {   // dev: the block record against the sum of its stage records
-            double tot = 0.0;
-            for (int j = 0; j < SLOG_BLOCK; ++j) {
-                const double a = samp_scale(Pw[j], rw[j] - R);
-                const double ao = __shfl_xor(a, 32);
-                if (j < sn) tot += hh == 0 ? a + ao : ao + a;
-            }
-            if (hh == 0 && fabs(tot - sblk) > 1e-9 * fabs(tot)) atomicAdd(p.stats + 1, 1000);
-        }
-#endif
         PROF_MARK(pm + 23);
         f32x16 x0, x1;
         samp_load_stage(lr, vo, SLOG_STAGE_BYTES * (uint32_t)sf, x0, x1);
@@ -1098,43 +1029,9 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
     else { tok = other; lpv = olp; }
 }
 
-#ifndef LOGIT_FLAGSYNC
-#define LOGIT_FLAGSYNC 0        // 1: the logit loop (G = 4) hands tiles over with per-wave LDS progress words
-#endif
-#define LSYNC_SPIN_TICKS 50000000ull   // 0.5 s of s_memrealtime for a progress wait (then stats[2], and on)
-
-// per-wave progress words of the logit loop (LOGIT_FLAGSYNC): the slowest of the 8 waves
-__device__ __forceinline__ int lsync_min8(const int* a) {
-    int m = 0x7fffffff;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) m = min(m, __hip_atomic_load(a + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    return m;
-}
-// wait until every wave's word reached `target` (LDS executes each wave's accesses in order, so the words
-// are set after the accesses they publish; the signal fences keep the compiler from moving LDS accesses across)
-__device__ __forceinline__ void lsync_wait(const int* a, int target, int32_t* stats) {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (lsync_min8(a) < target) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (lsync_min8(a) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > LSYNC_SPIN_TICKS) {
-                if (lane_fresh() == 0) atomicAdd(stats + 2, 1);
-                break;
-            }
-        }
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-__device__ __forceinline__ void lsync_set(int* a, int wave, int v) {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (lane_fresh() == 0) __hip_atomic_store(a + wave, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
-// HALF_LAST: the range's last stage runs chain a only when its rows 32-63 are all padding (the coop ranges: the
-// group waits for its slowest range, which holds the vocabulary's partial last stage)
-template <int G, bool PAIRS, class Tail = NoTail, class Hook = NoHook, bool HALF_LAST = false>
+// Measured and not kept (git history, r04): per-wave LDS progress words in place of the per-stage barrier (+0.4 %),
+// a chain-a-only last stage for the coop ranges (+1.3 % / +2.2 % at P = 64 / 128, or spills inside the loop).
+template <int G, bool PAIRS, class Tail = NoTail, class Hook = NoHook>
 __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, uint64_t nidx, int wave, int sgn,
                                              int hf, const float (&hB)[64], int s0, int s1, RowState& st,
                                              Stage64Regs& s64, bool preloaded = false, Tail&& tail = Tail(),
@@ -1162,17 +1059,11 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
     // so the end of a stage has no staging wait and no LDS-write tail in front of the barrier
     if (s0 + 1 < s1) stage64_load_o(lsrc(s0 + 1), lo, bias, s64);
 #endif
-    constexpr bool FS = LOGIT_FLAGSYNC && LOGIT_MIDSTORE && G == 4;
-    __shared__ int lsync[16];                     // FS: [0, 8) tiles written, [8, 16) stages read, per wave
-    if constexpr (FS) {
-        if (threadIdx.x < 16) lsync[threadIdx.x] = 0;
-    }
     __syncthreads();
     f32x16 a0, a1, b0, b1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { b0[r] = NEG_INF; b1[r] = NEG_INF; }
-    auto stage = [&](auto halfc, int s, f32x16& o0, f32x16& o1, const f32x16& q0, const f32x16& q1) {
-        constexpr bool HS = decltype(halfc)::value;    // HALF_LAST: this is the range's partial last stage
+    auto stage = [&](int s, f32x16& o0, f32x16& o1, const f32x16& q0, const f32x16& q1) {
         const int sn = min(s + 1, s1 - 1);
 #if !LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
         stage64_load_o(lsrc(sn), lo, bias, s64);
@@ -1185,10 +1076,7 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
             // s64 is loaded on every non-last path (at s1 - 2 the load repeats tile s1 - 1): a conditional load
             // here would make the compiler copy the 32 staging registers at every stage to merge the paths
             if (s + 1 < s1) {
-                // FS: the buffer was read in stage s - 1: every wave past it
-                if constexpr (FS) lsync_wait(lsync + 8, s - s0, p.stats);
                 stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
-                if constexpr (FS) lsync_set(lsync, wave, s + 1 - s0);
                 stage64_load_o(lsrc(min(s + 2, s1 - 1)), lo, bias, s64);
             } else {
                 tail();
@@ -1196,40 +1084,19 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
 #endif
         };
         constexpr int MID = LOGIT_MIDSTORE ? LOGIT_MID_AT : 9;   // 9: never
-        auto mm = [&]() __attribute__((always_inline)) {
-            if constexpr (FS) {                      // tile s written by every wave (tile s0: the barrier above)
-                if (s > s0) lsync_wait(lsync, s - s0, p.stats);
-            }
-            mfma_stage64_o<MID, HS>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
-            if constexpr (FS) lsync_set(lsync + 8, wave, s - s0 + 1);
-        };
         if constexpr (G == 4) {
             if (sgn == MFMA_FIRST_SIGN) {
+                mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
 #if !(DECODE_ABLATE & 1)
-                if constexpr (Hook::replaces && Hook::early) hook.template part<2>(q0, q1, s - 1);
-#endif
-                mm();
-#if !(DECODE_ABLATE & 1)
-                if constexpr (Hook::replaces) {
-                    if constexpr (Hook::early) hook.template part<5>(q0, q1, s - 1);
-                    else hook(q0, q1, s - 1);
-                } else {
-                    epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
-                }
+                if constexpr (Hook::replaces) hook(q0, q1, s - 1);
+                else epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
 #endif
             } else {
 #if !(DECODE_ABLATE & 1)
-                if constexpr (Hook::replaces) {
-                    if constexpr (Hook::split) hook.template part<1>(q0, q1, s - 1);
-                    else hook(q0, q1, s - 1);
-                } else {
-                    epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
-                }
+                if constexpr (Hook::replaces) hook(q0, q1, s - 1);
+                else epilogue64<PAIRS>(st, q0, q1, 64 * (s - 1) + vl);
 #endif
-                mm();
-#if !(DECODE_ABLATE & 1)
-                if constexpr (Hook::replaces && Hook::split) hook.template part<6>(q0, q1, s - 1);
-#endif
+                mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
             }
         } else {
             const float* w1 = wsg + 32 * hf * LDS_ROW;         // this wave's 32-row tile of the stage
@@ -1246,11 +1113,7 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
         stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
 #endif
 #if !(DECODE_ABLATE & 8)
-        if constexpr (FS) {
-            if (s == s1 - 1) __syncthreads();        // the phase after the loop reuses the buffers
-        } else {
-            __syncthreads();
-        }
+        __syncthreads();
 #endif
     };
     auto last = [&](const f32x16& q0, const f32x16& q1, int s) {
@@ -1261,44 +1124,15 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
             epilogue32<PAIRS>(st, q0, 64 * s + vl);
         }
     };
-    using F_ = std::false_type;
-    if constexpr (!HALF_LAST) {
-        for (int s = s0; s < s1; s += 2) {
-            stage(F_{}, s, a0, a1, b0, b1);
-            if (s + 1 == s1) {
-                last(a0, a1, s);
-                return;
-            }
-            stage(F_{}, s + 1, b0, b1, a0, a1);
-        }
-        last(b0, b1, s1 - 1);
-    } else {
-        // the partial last stage (rows 32-63 all padding) after the loop, as its own instantiation: inside the
-        // loop body its second MFMA form made the loop spill
-        const bool half = p.V1 - 64 * (s1 - 1) <= 32 && s1 - s0 >= 2;
-        const int se = half ? s1 - 1 : s1;
-        bool odd = false;
-        for (int s = s0; s < se; s += 2) {
-            stage(F_{}, s, a0, a1, b0, b1);
-            if (s + 1 == se) {
-                odd = true;
-                break;
-            }
-            stage(F_{}, s + 1, b0, b1, a0, a1);
-        }
-        if (!half) {
-            if (odd) last(a0, a1, se - 1);
-            else last(b0, b1, se - 1);
+    for (int s = s0; s < s1; s += 2) {
+        stage(s, a0, a1, b0, b1);
+        if (s + 1 == s1) {
+            last(a0, a1, s);
             return;
         }
-        if (odd) {
-            stage(std::true_type{}, se, b0, b1, a0, a1);
-            last(b0, b1, se);
-        } else {
-            stage(std::true_type{}, se, a0, a1, b0, b1);
-            last(a0, a1, se);
-        }
+        stage(s + 1, b0, b1, a0, a1);
     }
+    last(b0, b1, s1 - 1);
 }
 
 // gate tiles of the cell: tile m = 0..19 is gate chunk tile_q(m) (order g1, g2, i, f, o) of the
@@ -1613,11 +1447,11 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         };
         // SAMPLE: the lane's running max, reference and sum of terms (SampleStage), the logits to the slot
         float sm = -1.0e30f, sref = -1.0e30f;
-        double sT = 0.0, sB = 0.0, sP = 0.0;
+        double sT = 0.0, sB = 0.0;
         if constexpr (SAMPLE) {
             const SampleStage ss{c.slog_r, 16u * (uint32_t)lane_fresh() + SLOG_WAVE_BYTES * (uint32_t)c.wave,
                                  16u * (uint32_t)lane_fresh() + 1024u * (uint32_t)c.wave, (p.V1 + 63) >> 6, sm, sref, sT,
-                                 sB, sP};
+                                 sB};
             logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail, ss);
         } else {
             logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail);
@@ -2322,8 +2156,7 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         auto tail = [&]() __attribute__((always_inline)) {
             if (CROSS_PREFETCH && t < p.T) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
         };
-        logit_stages<4, PAIRS, decltype(tail)&, NoHook, COOP_HALF_LAST>(lds, p, nidx, c.wave, c.sgn, 0, hB, s0, s1, st, s64,
-                                                                        pre && LOGIT_MIDSTORE, tail);
+        logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, s0, s1, st, s64, pre && LOGIT_MIDSTORE, tail);
         cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && t < p.T;
         PROF_AT(blockIdx.x, 1024, pm + 1);
         // ---- phase A: this range's partial greedy state, write-through, then the group's merge
