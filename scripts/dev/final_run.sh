@@ -1,6 +1,6 @@
 set -eo pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/final2; mkdir -p $O
+O=gpurun_out/final3; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
 timeout -k 10 400 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err
