@@ -56,3 +56,23 @@ def test_presets_name_the_baseline_configs():
     assert bench.PRESETS['configs1'][0] == 64 and 'pop=64' in cfgs[1]
     assert bench.PRESETS['configs3'][0] == 2048 and 'pop=2048' in cfgs[3]
     assert bench.PRESETS['configs4'][2] and 'bu' in cfgs[4] and 'pop=512' in cfgs[4]
+
+
+def test_committed_pmc_profiles_match_the_decode_sources():
+    """The bench line's counter figures (traffic, MFMA busy) come from committed PMC profiles: every shape the
+    bench reports (the fused kernel at 512 and 256 members per GPU, the coop kernel at 128 and 64, the sampled
+    kernel) has one recorded against the current decode sources."""
+    for kernel, P in (('nicnes_decode_steps_kernel', 512), ('nicnes_decode_coop_kernel<2>', 128),
+                      ('nicnes_decode_coop_kernel<4>', 64), ('nicnes_decode_steps_kernel<sample>', 512)):
+        rec, why = bench.load_pmc(kernel, P, 128)
+        assert rec is not None, why
+        assert rec['derived']['hbm_bytes_per_launch'] > 0 and 0 < rec['derived']['mfma_busy'] < 1
+
+
+def test_sampled_slot_bytes_follow_the_slot_layout():
+    """bench.py's sampled algorithmic bytes: per workgroup, logit step and 64-row stage 72 KiB (8 logit words and
+    the {P, r} record, 9 x 64 lanes x 16 B per wave, 8 waves) plus 8 KiB per block of 8 stages."""
+    nst = (9488 + 63) // 64
+    assert nst == 149 and 9 * 64 * 16 * 8 == 73728
+    src = open(os.path.join(bench.REPO, 'bench.py')).read()
+    assert 'nst * 73728 + (nst + 7) // 8 * 8192' in src
