@@ -14,11 +14,20 @@ configs4 ('bu' features, pop=512; 64 per GPU on 8). --pop-per-gpu M is weak scal
 
     python bench.py [--gpus N --steps K --warmup W] [--preset metric|configs1|configs2|configs3|configs4]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+--gpus N without a launcher (no WORLD_SIZE in the environment) starts N rank processes itself, before
+anything touches the GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set
+as torch.distributed.run sets them, and exits with the first failing rank's status. Under a launcher
+--gpus must equal WORLD_SIZE (exit 2 otherwise: a one-GPU number is never printed as an N-GPU one).
+The line records what the collective saw (dist.get_world_size(); ncclCommCount with --comm engine) and
+every rank's member range and decode / exchange / update times.
 """
 import hashlib
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -170,9 +179,94 @@ def cpu_baseline(args, B, P):
                                     'rate (linear, an upper bound for the reference)'}
 
 
+def resolve_world(gpus, env):
+    """(world, launched_here): the rank count this run uses. `gpus` is --gpus (None: not given).
+    Under a launcher (WORLD_SIZE set) --gpus must name the same count; without one, --gpus N > 1 means
+    this process starts the N ranks itself (launched_here True). Raises SystemExit(2) on a mismatch."""
+    ws = env.get('WORLD_SIZE')
+    if ws is not None:
+        world = int(ws)
+        if gpus is not None and gpus != world:
+            print('bench.py: --gpus %d but WORLD_SIZE=%d: refusing to report a %d-rank run as %d GPUs'
+                  % (gpus, world, world, gpus), file=sys.stderr, flush=True)
+            raise SystemExit(2)
+        return world, False
+    n = 1 if gpus is None else int(gpus)
+    if n < 1:
+        raise SystemExit(2)
+    return n, n > 1
+
+
+def rank_environments(n, port, base):
+    """The environment of each of the n rank processes, as torch.distributed.run sets it on one node."""
+    out = []
+    for r in range(n):
+        env = dict(base)
+        env.update({'RANK': str(r), 'LOCAL_RANK': str(r), 'WORLD_SIZE': str(n), 'LOCAL_WORLD_SIZE': str(n),
+                    'GROUP_RANK': '0', 'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port),
+                    'HSA_ENABLE_IPC_MODE_LEGACY': base.get('HSA_ENABLE_IPC_MODE_LEGACY', '0')})
+        out.append(env)
+    return out
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, grace=30.0):
+    """Start n fresh rank processes running this script with `argv` (this process never touches the
+    GPU), wait for all of them, and return the exit status: 0, or the first failing rank's (a rank
+    killed by a signal counts as 1). When one rank fails the others are terminated."""
+    shared = os.environ.get('NICNES_BENCH_SHARE_GPU') == '1'
+    if not shared:
+        import torch
+        have = torch.cuda.device_count()          # counts devices without initialising HIP
+        if have < n:
+            print('bench.py: --gpus %d but %d GPUs are visible' % (n, have), file=sys.stderr, flush=True)
+            return 2
+    port = free_port()
+    # rank 0's JSON line is the only stdout; everything else the ranks print (gloo / RCCL banners,
+    # rank > 0) goes to stderr
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                              stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(), text=r == 0)
+             for r, env in enumerate(rank_environments(n, port, os.environ))]
+
+    def forward(pipe):
+        for line in pipe:
+            (sys.stdout if line.startswith('{') else sys.stderr).write(line)
+            (sys.stdout if line.startswith('{') else sys.stderr).flush()
+    import threading
+    fw = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
+    fw.start()
+    rc, alive, t_fail = 0, list(procs), None
+    while alive:
+        for p in list(alive):
+            r = p.poll()
+            if r is None:
+                continue
+            alive.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 1
+                t_fail = time.time()
+                for q in alive:
+                    q.terminate()
+        if alive and t_fail is not None and time.time() - t_fail > grace:
+            for q in alive:
+                q.kill()
+        time.sleep(0.1)
+    fw.join(timeout=10)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=None, help='GPUs (= ranks); without a launcher this process '
+                    'starts them (default: WORLD_SIZE, or 1)')
+    ap.add_argument('--comm', choices=['torch', 'engine'], default='torch', help="the exchange's binding: "
+                    "torch.distributed (RCCL as the 'nccl' backend) or the engine's own RCCL communicator "
+                    "(nicnes_comm_init; its id shared over a gloo group)")
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--preset', choices=sorted(PRESETS), default='metric', help='BASELINE.json config')
@@ -204,7 +298,17 @@ def main():
     ap.add_argument('--cpu-members-per-core', type=int, default=1)
     args = ap.parse_args()
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
+    world, launch_here = resolve_world(args.gpus, os.environ)
+    if launch_here:
+        raise SystemExit(launch_ranks(world, sys.argv[1:]))
+    if os.environ.get('NICNES_BENCH_DRY_RANKS') == '1':
+        # test hook (tests/test_bench_launcher.py): report the rank environment and stop before any GPU work
+        print(json.dumps({k: os.environ.get(k) for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR',
+                                                          'MASTER_PORT')}), flush=True)
+        fail = os.environ.get('NICNES_BENCH_DRY_FAIL_RANK')
+        if fail is not None and fail == os.environ.get('RANK'):
+            raise SystemExit(3)
+        return
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     P_pre, B_pre, bu_pre, cfg_text = PRESETS[args.preset]
@@ -232,14 +336,22 @@ def main():
 
     # rehearsal knobs for a one-GPU box (never set by the driver): every rank on cuda:0 over gloo
     backend = os.environ.get('NICNES_BENCH_BACKEND', 'nccl')
-    dev = 0 if os.environ.get('NICNES_BENCH_SHARE_GPU') == '1' else local_rank
+    share_gpu = os.environ.get('NICNES_BENCH_SHARE_GPU') == '1'
+    dev = 0 if share_gpu else local_rank
     torch.cuda.set_device(dev)
     group = None
     if world > 1:
+        if args.comm == 'engine':
+            backend = 'gloo'                 # the bootstrap group: the data plane is the engine's communicator
         if backend == 'nccl':
             dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world or dist.get_rank() != rank:
+            raise SystemExit('torch.distributed formed %d ranks (rank %d), expected %d (rank %d)'
+                             % (dist.get_world_size(), dist.get_rank(), world, rank))
+    # host tensors for the bench's own barrier / max-reduce on a gloo group, device tensors on RCCL
+    red_dev = 'cuda' if (world > 1 and backend == 'nccl') else 'cpu'
     sampled = args.fitness in ('sample', 'self_critical', 'sc_loss')
     spi = 5 if sampled else 1               # sampled modes decode the reference's seq_per_img copies of each image
     eng = nicnes.Engine(max_batch=B, max_members=P_local, noise_len=args.noise_len, noise_seed=0, device=dev)
@@ -249,8 +361,17 @@ def main():
     if sampled:
         eng.set_rows_per_image(spi)          # each image's 5 copies decoded, each with its own draws
     eng.set_decode_split(args.decode_split, args.decode_rows)
+    if share_gpu and world > 1:
+        # ranks time-sharing one GPU (rehearsal only): the coop decode assumes the whole device
+        eng.set_decode_coop(0)
+    comm = None
+    if world > 1 and args.comm == 'engine':
+        uid = [nicnes.Engine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(world, rank, uid[0])
+        comm = 'engine'
     runner = PopulationRunner(eng, P, args.sigma, l2coeff=1e-7, stepsize=1e-3, rank=rank, world_size=world,
-                              group=group)
+                              group=group, comm=comm)
     mut_s = []
     if args.mutation:
         # SM-G-SUM: Sensitivity.calc_sensitivity of the task's theta on its batch (safe_mutations.py:34-117),
@@ -278,14 +399,25 @@ def main():
         it += 1
     eng.set_timing(True)
     dec_ms, phases = [], []
+    # per timed step: events on the engine's stream (torch's current stream) between the iteration's
+    # three parts -- evaluate (decode + CIDEr-D), the fitness exchange, update (ranks, noise sum, its
+    # all-reduce, Adam); runner.step issues exactly these calls
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     mut_s.clear()
-    for _ in range(args.steps):
+    for k in range(args.steps):
         prepare(it)                                            # host sensitivity (waits for the last theta)
-        runner.step(it, sync=False, n_batches=args.batches)   # enqueue only (a batch map is one small copy)
+        e = evs[k]
+        e[0].record()
+        runner.evaluate(it, args.batches)                      # enqueue only (a batch map is one small copy)
+        e[1].record()
+        runner.exchange_fitness()
+        e[2].record()
+        runner.update(it, sync=False)
+        e[3].record()
         it += 1
     torch.cuda.synchronize()
     if world > 1:
@@ -295,10 +427,27 @@ def main():
     # decode timing of the last timed step (HIP events recorded between its launches)
     dec_ms.append(eng.kernel_times()[0])
     phases.append(eng.decode_phase_times())
+    part_ms = [float(np.mean([e[j].elapsed_time(e[j + 1]) for e in evs])) for j in range(3)]
+    mine = [rank, runner.m0, runner.m0 + runner.local, dev, dt * 1e3 / args.steps] + part_ms
+    ranks = [mine]
+    comm_seen = {'binding': 'none (one rank)' if world == 1 else
+                 ('engine RCCL communicator (nicnes_comm_init)' if comm == 'engine' else
+                  'torch.distributed %s' % backend),
+                 'world_size': dist.get_world_size() if world > 1 else 1}
+    if comm == 'engine':
+        comm_seen['rccl_comm_count'], comm_seen['rccl_rank'] = eng.comm_count()
     if world > 1:
-        t = torch.tensor([dt], device='cuda')
+        t = torch.tensor([dt], device=red_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        row = torch.tensor(mine, device=red_dev, dtype=torch.float64)
+        rows = [torch.zeros_like(row) for _ in range(world)]
+        dist.all_gather(rows, row)
+        ranks = [r.cpu().tolist() for r in rows]
+        if comm == 'engine':
+            n_seen = torch.tensor([comm_seen['rccl_comm_count']], device=red_dev, dtype=torch.float64)
+            dist.all_reduce(n_seen, op=dist.ReduceOp.MIN)
+            comm_seen['rccl_comm_count_min_over_ranks'] = int(n_seen.item())
     value = P * args.steps / dt
     mut_ms = float(np.mean([a.elapsed_time(b) for a, b in mut_s])) if mut_s else 0.0
     dec_s = float(np.mean(dec_ms)) / 1e3
@@ -383,7 +532,12 @@ def main():
                    'vocab_size': 9487,
                    'parallelism': ('none (one GPU, no collective)' if world == 1 else
                                    'population-sharded x%d, %s all-gather of fitness + all-reduce of the noise sum'
-                                   % (world, 'RCCL' if backend == 'nccl' else backend))},
+                                   % (world, 'RCCL' if (backend == 'nccl' or comm == 'engine') else backend)),
+                   'collective': comm_seen,
+                   'shared_gpu_rehearsal': bool(share_gpu and world > 1)},
+        'ranks': [{'rank': int(r[0]), 'members': [int(r[1]), int(r[2])], 'device': int(r[3]),
+                   'ms_per_step': round(r[4], 3), 'evaluate_ms': round(r[5], 3), 'exchange_ms': round(r[6], 3),
+                   'update_ms': round(r[7], 3)} for r in ranks],
         'roofline': {'bound': 'mfma', 'kernel': kname, 'achieved': round(achieved, 3),
                      'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                      'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic,

@@ -26,6 +26,7 @@ extern "C" {
 #define NICNES_ERR_UNSUPPORTED 2   /* experiment option the engine does not implement */
 #define NICNES_ERR_HIP 3           /* HIP runtime error (message in nicnes_last_error) */
 #define NICNES_ERR_NOMEM 4
+#define NICNES_ERR_FAULT 5         /* contained decode fault: NaN fitness, the optimizer step skipped (nicnes_stats) */
 
 typedef struct nicnes_handle nicnes_handle;
 
@@ -226,12 +227,17 @@ int nicnes_optimizer_update(nicnes_handle* h, int kind, const double* globalg, i
  * 92-123,170-182); the engine exchanges the (P, 2) fitness and one D-float noise sum over RCCL.
  * nicnes_comm_unique_id: rank 0 makes the 128-byte id and sends it to the other ranks out of band;
  * nicnes_comm_init: every rank joins (collective, blocking); nicnes_comm_attach borrows an
- * ncclComm_t the caller already owns (e.g. torch.distributed's); nicnes_comm_destroy releases. */
+ * ncclComm_t the caller already owns (e.g. torch.distributed's); nicnes_comm_destroy releases.
+ * nicnes_comm_count: the rank count and this rank's index as RCCL itself reports them
+ * (ncclCommCount / ncclCommUserRank on the bound communicator; 1 and 0 with none bound) -- what a
+ * multi-GPU bench line records to prove the collective saw N ranks (the reference's counterpart is
+ * the number of live worker processes, src/main.py:144-153). */
 #define NICNES_COMM_ID_BYTES 128
 int nicnes_comm_unique_id(uint8_t* id_out_host);
 int nicnes_comm_init(nicnes_handle* h, int32_t nranks, int32_t rank, const uint8_t* id_host);
 int nicnes_comm_attach(nicnes_handle* h, void* nccl_comm);
 int nicnes_comm_destroy(nicnes_handle* h);
+int nicnes_comm_count(nicnes_handle* h, int32_t* nranks_out_host, int32_t* rank_out_host);
 /* fit_all [P_local * nranks, 2] fp64 <- every rank's fit_local [P_local, 2], in rank order, so every
  * rank then ranks the whole population identically (compute_centered_ranks needs all 2P values). */
 int nicnes_allgather_fitness(nicnes_handle* h, const double* fit_local, int32_t P_local, double* fit_all, void* stream);
@@ -245,11 +251,20 @@ int nicnes_allreduce_grad(nicnes_handle* h, float* gsum, void* stream);
  * Decode faults ([2] or [3] nonzero: rows left undecoded) are sticky and contained on the device, in the
  * iteration that hit them, without a host wait: every fitness written from then on is NaN, nicnes_grad_partial
  * writes NaN everywhere (so an all-reduce carries the fault to every rank), and an optimizer step on this handle,
- * or on a noise sum whose first entry is NaN, leaves theta, m and v untouched. The error (NICNES_ERR_HIP) is
+ * or on a noise sum whose first entry is NaN, leaves theta, m and v untouched. The error (NICNES_ERR_FAULT) is
  * returned by the next evaluate that finds the counters read back, and by the ratio read of the skipped step
- * (nicnes_adam_step / nicnes_sgd_step with ratio_out_host, nicnes_last_ratio). The handle stays faulted:
- * destroy it (the reference's worker process dies and is restarted, main.py:107-141). */
+ * (nicnes_adam_step / nicnes_sgd_step with ratio_out_host, nicnes_last_ratio); a skipped step is known by
+ * the Adam kernel's own skip flag, so the NaN ratio of an applied step (0/0) is returned as a ratio, not an
+ * error. The handle stays faulted until nicnes_clear_faults, or destroy it (the reference's worker process
+ * dies and is restarted, main.py:107-141). */
 int nicnes_stats(nicnes_handle* h, int64_t* out4_host);
+
+/* Clear a contained decode fault (synchronising on the device): out2_host (nullable) receives the fault
+ * counters [2], [3] of nicnes_stats before they are zeroed; the logit-slot claim flags are reset. theta, m
+ * and v are those from before the faulted iteration (its step was skipped), so a caller can re-run that
+ * iteration on the same handle (nicnes.master.EngineMaster.run does, once). Not a reference interface: the
+ * reference's recovery is a fresh worker process (main.py:107-141). */
+int nicnes_clear_faults(nicnes_handle* h, int64_t* out2_host);
 
 /* Kernel timing with HIP events recorded on the launch stream around the decode and CIDEr-D
  * launches of nicnes_evaluate (off by default). nicnes_kernel_times synchronises on the events

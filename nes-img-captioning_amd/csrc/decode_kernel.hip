@@ -56,6 +56,9 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #define CELL_SIG(x) nn_sigmoidf(x)
 #define CELL_TANH(x) nn_tanhf(x)
 #endif
+#ifndef NICNES_STORE_WAITS
+#define NICNES_STORE_WAITS 1  // the product: wait states after the sampled pick's 16-byte record stores (gfx950
+#endif                        // store-data hazard); 0 only in the scan's scratch build (tests/test_isa_hazards.py)
 #ifndef MFMA_FIRST_SIGN
 #define MFMA_FIRST_SIGN 0  // logit stages: the sign whose waves run the stage's MFMAs before the previous epilogue
 #endif
@@ -841,7 +844,9 @@ struct SampleStage {
             const uint64_t pb = __builtin_bit_cast(uint64_t, P);
             const u32x4 w = {(uint32_t)pb, (uint32_t)(pb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
             __builtin_amdgcn_raw_buffer_store_b128(w, slot, (int)vo, (int)(so + 8u * 1024u), SLOG_STORE_POLICY);
+#if NICNES_STORE_WAITS
             asm volatile("s_nop 1" ::"v"(w));                // (the wait states of the block record below)
+#endif
             if ((s % SLOG_BLOCK) == SLOG_BLOCK - 1 || s == nst - 1) {      // the block's record (wave-uniform branch)
                 const uint64_t bb = __builtin_bit_cast(uint64_t, Bk);
                 const u32x4 wb = {(uint32_t)bb, (uint32_t)(bb >> 32), __builtin_bit_cast(uint32_t, ref), 0u};
@@ -851,7 +856,9 @@ struct SampleStage {
                 // the 16-byte store reads its data registers after issue: the compiler put the zeroing of Bk
                 // right behind it with no wait state and lanes 12-15 of each 16 stored 0 (gfx950, measured); the
                 // asm keeps Bk's registers unwritten for two wait states
+#if NICNES_STORE_WAITS
                 asm volatile("s_nop 1" : "+v"(Bk));
+#endif
                 Bk = 0.0;
             }
         }

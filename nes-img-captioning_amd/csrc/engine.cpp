@@ -121,6 +121,7 @@ struct nicnes_handle {
     // only the runtime's check of that bound) and costs 0.4 % less per iteration at P = 64 (r04 A/B)
     int coop_launch = 0;
     uint32_t test_stall_ms = 0;       // test hook NICNES_TEST_COOP_STALL (ms): coop workgroup 0 starts late
+    int test_stall_left = -1;         // ... on the first NICNES_TEST_COOP_STALL_LAUNCHES coop launches only (-1: all)
     int test_slots = 0;               // test hook NICNES_TEST_SLOTS: this many sampled logit slots (0 = enough)
     uint32_t* coop_ctr = nullptr;     // [max_members * slabs * COOP_CTR_STRIDE] coop hand-off counters
     SensWork* sens = nullptr;         // SM-G-SUM sensitivity work buffers (nicnes_sum_sensitivity)
@@ -156,6 +157,11 @@ struct nicnes_handle {
     int n_dev = 0;                            // events recorded by the last timed decode
     bool multi_stream = false;                // the last decode ran on several streams
     bool last_nes_form = true;                // the newest optimizer step took the noise sum (not a globalg)
+    // a skipped step (the Adam kernel's skip flag) leaves theta, m, v untouched; the host state it advanced
+    // (t, theta_is_fp32) is rolled back once the flag is seen, so a re-run of the iteration steps as the first try would
+    bool step_pending_check = false;
+    int64_t t_prev = 0;
+    int theta_fp32_prev = 0;
 };
 
 namespace {
@@ -369,6 +375,8 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
         if (cl && (cl[0] == '0' || cl[0] == '1') && cl[1] == 0) h->coop_launch = cl[0] - '0';
         const char* st = getenv("NICNES_TEST_COOP_STALL");
         if (st && st[0]) h->test_stall_ms = (uint32_t)atoi(st);
+        const char* sl = getenv("NICNES_TEST_COOP_STALL_LAUNCHES");
+        if (sl && sl[0]) h->test_stall_left = atoi(sl);
         const char* ts = getenv("NICNES_TEST_SLOTS");
         if (ts && ts[0]) h->test_slots = atoi(ts);
     }
@@ -387,7 +395,7 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
     if (!rc && hipEventCreateWithFlags(&h->stats_ev, hipEventDisableTiming) != hipSuccess)
         rc = fail(h, NICNES_ERR_HIP, "hipEventCreate");
     if (!rc) rc = dalloc(h, &h->partials, 2 * (size_t)nicnes_adam_blocks(h->D));
-    if (!rc) rc = dalloc(h, &h->norms, 2);
+    if (!rc) rc = dalloc(h, &h->norms, 3);       // |step|^2, |theta|^2, the skip flag
     if (!rc) {
         h->rank_cap = nicnes_rank_scratch_pairs(2 * cfg->max_members);
         rc = dalloc(h, &h->rank_key, h->rank_cap);
@@ -477,6 +485,7 @@ int nicnes_set_theta(nicnes_handle* h, const double* theta64, int is_fp32_origin
                        h->theta32, h->D);
     HIPC(h, hipGetLastError());
     h->theta_is_fp32 = is_fp32_origin ? 1 : 0;
+    h->step_pending_check = false;
     h->theta_set = true;
     return NICNES_OK;
 }
@@ -499,6 +508,7 @@ int nicnes_set_adam_state(nicnes_handle* h, const double* m, const double* v, in
     HIPC(h, hipMemcpyAsync(h->m, m, (size_t)h->D * sizeof(double), hipMemcpyDeviceToDevice, s));
     HIPC(h, hipMemcpyAsync(h->v, v, (size_t)h->D * sizeof(double), hipMemcpyDeviceToDevice, s));
     h->t = t;
+    h->step_pending_check = false;
     return NICNES_OK;
 }
 
@@ -825,9 +835,9 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     if (h->stats_pending && hipEventQuery(h->stats_ev) == hipSuccess) {   // the last decode's fallbacks
         const int32_t fb = h->stats_host[0];
         if (h->stats_host[2] != 0)
-            return fail(h, NICNES_ERR_HIP, "coop decode: a workgroup's partners never arrived (hand-off timeout)");
+            return fail(h, NICNES_ERR_FAULT, "coop decode: a workgroup's partners never arrived (hand-off timeout)");
         if (h->stats_host[3] != 0)
-            return fail(h, NICNES_ERR_HIP, "sampled decode: a workgroup found no free logit slot");
+            return fail(h, NICNES_ERR_FAULT, "sampled decode: a workgroup found no free logit slot");
         if (h->last_bounded && fb - h->fb_seen >= 2) h->exact_left = 32;
         h->fb_seen = fb;
         h->stats_pending = false;
@@ -889,7 +899,8 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     p.part = h->part;
     p.coop = !sampled && coop_fits(h, G, nslabs, S, count) ? 1 : 0;
     p.coop_launch = h->coop_launch;
-    p.test_stall_ms = h->test_stall_ms;
+    p.test_stall_ms = h->test_stall_left != 0 ? h->test_stall_ms : 0;
+    if (p.coop && h->test_stall_ms && h->test_stall_left > 0) --h->test_stall_left;
     // log-probs of a batch spread over several slabs: every slab runs to T, then the steps after the
     // batch's last finishing step are zeroed (nicnes_lp_batch_exit), as FCModel._sample leaves them
     p.no_exit = (p.lp && nslabs > 1) ? 1 : 0;
@@ -1089,12 +1100,20 @@ int nicnes_grad_partial_range(nicnes_handle* h, uint64_t iteration, int32_t memb
 static int fault_error(nicnes_handle* h, bool from_noise_sum = true) {
     int32_t st[4];
     HIPC(h, hipMemcpy(st, h->stats, sizeof st, hipMemcpyDeviceToHost));
-    if (st[2] != 0) return fail(h, NICNES_ERR_HIP, "coop decode: a workgroup's partners never arrived (hand-off timeout); "
-                                                   "the iteration's fitness is NaN and the optimizer step was skipped");
-    if (st[3] != 0) return fail(h, NICNES_ERR_HIP, "sampled decode: a workgroup found no free logit slot; "
-                                                   "the iteration's fitness is NaN and the optimizer step was skipped");
+    if (st[2] != 0) return fail(h, NICNES_ERR_FAULT, "coop decode: a workgroup's partners never arrived (hand-off timeout); "
+                                                     "the iteration's fitness is NaN and the optimizer step was skipped");
+    if (st[3] != 0) return fail(h, NICNES_ERR_FAULT, "sampled decode: a workgroup found no free logit slot; "
+                                                     "the iteration's fitness is NaN and the optimizer step was skipped");
     if (!from_noise_sum) return NICNES_OK;      // Optimizer.update(globalg) with a NaN globalg: as the reference
-    return fail(h, NICNES_ERR_HIP, "optimizer step skipped: the noise sum is NaN (a faulted decode on another rank)");
+    return fail(h, NICNES_ERR_FAULT, "optimizer step skipped: the noise sum is NaN (a faulted decode on another rank)");
+}
+
+// the newest step was skipped (its flag read back as set): undo its host-side state once
+static void rollback_skipped_step(nicnes_handle* h) {
+    if (!h->step_pending_check) return;
+    h->t = h->t_prev;
+    h->theta_is_fp32 = h->theta_fp32_prev;
+    h->step_pending_check = false;
 }
 
 // one optimizer update (kind 0 Adam, 1 SGD), from the fused NES form (gsum, P, l2coeff) or from a
@@ -1104,6 +1123,9 @@ static int opt_step(nicnes_handle* h, int kind, const float* gsum, int32_t P, do
     if (!h->theta_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_theta first");
     hipStream_t s = (hipStream_t)stream;
     HIPC(h, hipSetDevice(h->device));
+    h->t_prev = h->t;
+    h->theta_fp32_prev = h->theta_is_fp32;
+    h->step_pending_check = true;
     h->t += 1;
     AdamParams p;
     p.theta64 = h->theta64;
@@ -1132,15 +1154,20 @@ static int opt_step(nicnes_handle* h, int kind, const float* gsum, int32_t P, do
     p.one_minus_beta2_32 = (float)(1.0 - b2);
     p.epsilon = epsilon;
     p.fault = h->stats;
+    p.skip_out = h->norms + 2;
     h->last_nes_form = globalg == nullptr;
     HIPC(h, nicnes_launch_adam(&p, h->norms, s));
     h->theta_is_fp32 = 0;
     if (ratio_out_host) {
-        double n2[2];
-        HIPC(h, hipMemcpyAsync(n2, h->norms, sizeof n2, hipMemcpyDeviceToHost, s));
+        double n3[3];
+        HIPC(h, hipMemcpyAsync(n3, h->norms, sizeof n3, hipMemcpyDeviceToHost, s));
         HIPC(h, hipStreamSynchronize(s));
-        *ratio_out_host = std::sqrt(n2[0]) / std::sqrt(n2[1]);
-        if (std::isnan(*ratio_out_host)) return fault_error(h, globalg == nullptr);
+        *ratio_out_host = std::sqrt(n3[0]) / std::sqrt(n3[1]);
+        if (n3[2] != 0.0) {
+            rollback_skipped_step(h);
+            return fault_error(h, globalg == nullptr);
+        }
+        h->step_pending_check = false;
     }
     return NICNES_OK;
 }
@@ -1150,11 +1177,41 @@ int nicnes_last_ratio(nicnes_handle* h, double* ratio_out_host, void* stream) {
     if (h->t == 0) return fail(h, NICNES_ERR_INVALID, "no optimizer step yet");
     hipStream_t s = (hipStream_t)stream;
     HIPC(h, hipSetDevice(h->device));
-    double n2[2];
-    HIPC(h, hipMemcpyAsync(n2, h->norms, sizeof n2, hipMemcpyDeviceToHost, s));
+    double n3[3];
+    HIPC(h, hipMemcpyAsync(n3, h->norms, sizeof n3, hipMemcpyDeviceToHost, s));
     HIPC(h, hipStreamSynchronize(s));
-    *ratio_out_host = std::sqrt(n2[0]) / std::sqrt(n2[1]);
-    if (std::isnan(*ratio_out_host)) return fault_error(h, h->last_nes_form);
+    *ratio_out_host = std::sqrt(n3[0]) / std::sqrt(n3[1]);
+    if (n3[2] != 0.0) {
+        rollback_skipped_step(h);
+        return fault_error(h, h->last_nes_form);
+    }
+    h->step_pending_check = false;
+    return NICNES_OK;
+}
+
+int nicnes_clear_faults(nicnes_handle* h, int64_t* counters_out_host) {
+    if (!h) return NICNES_ERR_INVALID;
+    HIPC(h, hipSetDevice(h->device));
+    HIPC(h, hipDeviceSynchronize());            // every launch that could still count has finished
+    int32_t st[4];
+    HIPC(h, hipMemcpy(st, h->stats, sizeof st, hipMemcpyDeviceToHost));
+    if (h->step_pending_check) {                 // the newest step's skip flag was not read yet
+        double skip = 0.0;
+        HIPC(h, hipMemcpy(&skip, h->norms + 2, sizeof skip, hipMemcpyDeviceToHost));
+        if (skip != 0.0) rollback_skipped_step(h);
+        else h->step_pending_check = false;
+    }
+    if (counters_out_host) {
+        counters_out_host[0] = st[2];
+        counters_out_host[1] = st[3];
+    }
+    // zero the fault words only (the fallback counters [0], [1] keep counting) and the logit-slot claim flags
+    // (the coop hand-off counters are zeroed before every coop launch), then forget the pending read-back
+    // that carried the fault
+    HIPC(h, hipMemset(h->stats + 2, 0, 2 * sizeof(int32_t)));
+    if (h->slog_slots) HIPC(h, hipMemset(h->slog_slots, 0, (size_t)h->slog_ns * sizeof(int32_t)));
+    HIPC(h, hipDeviceSynchronize());
+    h->stats_pending = false;
     return NICNES_OK;
 }
 
@@ -1330,6 +1387,18 @@ int nicnes_comm_destroy(nicnes_handle* h) {
     h->comm = nullptr;
     h->comm_owned = false;
     h->comm_nranks = 1;
+    return NICNES_OK;
+}
+
+int nicnes_comm_count(nicnes_handle* h, int32_t* nranks_out_host, int32_t* rank_out_host) {
+    if (!h || !nranks_out_host || !rank_out_host) return NICNES_ERR_INVALID;
+    int n = 1, r = 0;
+    if (h->comm) {
+        NCCLC(h, ncclCommCount(h->comm, &n));
+        NCCLC(h, ncclCommUserRank(h->comm, &r));
+    }
+    *nranks_out_host = n;
+    *rank_out_host = r;
     return NICNES_OK;
 }
 

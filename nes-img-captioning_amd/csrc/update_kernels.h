@@ -23,6 +23,7 @@ struct AdamParams {
     const double* globalg;  // non-null: Optimizer.update(globalg) form (gsum / l2coeff unused)
     int32_t g_is_fp32;      // globalg was an fp32 array: (1 - b) * g' products stay fp32 (NEP 50)
     const int32_t* fault;   // nullable: the handle's decode counters (decode_fault: the step is skipped)
+    double* skip_out;       // 1.0 when this step was skipped (a fault), 0.0 when applied
 };
 
 extern "C" hipError_t nicnes_launch_noise_index(uint64_t seed, uint64_t iteration, uint64_t member0, int count,

@@ -173,6 +173,9 @@ __global__ __launch_bounds__(256) void nicnes_adam_kernel(AdamParams p) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double s2 = 0.0, t2 = 0.0;
     const bool skip = decode_fault(p.fault) || (p.gsum != nullptr && p.gsum[0] != p.gsum[0]);
+    // the explicit skip flag beside the norms (norms[2]): the host raises the fault error only when it is set,
+    // not for a NaN ratio of an applied step (0/0 at theta = step = 0, or a NaN entry past index 0)
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.skip_out[0] = skip ? 1.0 : 0.0;
     if (skip) {
         s2 = t2 = __builtin_nan("");
     } else if (j < p.dim) {

@@ -5,10 +5,10 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libnicnes.so')
 
-OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_HIP, ERR_NOMEM = 0, 1, 2, 3, 4
+OK, ERR_INVALID, ERR_UNSUPPORTED, ERR_HIP, ERR_NOMEM, ERR_FAULT = 0, 1, 2, 3, 4, 5
 COMM_ID_BYTES = 128
 _NAMES = {ERR_INVALID: 'invalid argument', ERR_UNSUPPORTED: 'not supported', ERR_HIP: 'HIP error',
-          ERR_NOMEM: 'out of device memory'}
+          ERR_NOMEM: 'out of device memory', ERR_FAULT: 'contained decode fault'}
 
 # every symbol include/nicnes.h declares (checked by tests/test_abi.py)
 EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicnes_destroy', 'nicnes_last_error',
@@ -18,7 +18,7 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_set_timing', 'nicnes_kernel_times', 'nicnes_decode_phase_times', 'nicnes_sgd_step',
            'nicnes_optimizer_update', 'nicnes_last_ratio', 'nicnes_set_fitness_mode', 'nicnes_evaluate_lp',
            'nicnes_set_decode_split', 'nicnes_decode_shape', 'nicnes_set_decode_streams', 'nicnes_comm_unique_id', 'nicnes_comm_init',
-           'nicnes_comm_attach', 'nicnes_comm_destroy', 'nicnes_allgather_fitness', 'nicnes_allreduce_grad',
+           'nicnes_comm_attach', 'nicnes_comm_destroy', 'nicnes_comm_count', 'nicnes_clear_faults', 'nicnes_allgather_fitness', 'nicnes_allreduce_grad',
            'nicnes_noise_vectors', 'nicnes_set_batches', 'nicnes_evaluate_batches', 'nicnes_set_mutation',
            'nicnes_set_decode_coop', 'nicnes_decode_path', 'nicnes_sum_sensitivity', 'nicnes_grad_partial_range',
            'nicnes_evaluate_theta', 'nicnes_set_sample_draws', 'nicnes_set_rows_per_image']
@@ -33,6 +33,12 @@ class NicnesConfig(ctypes.Structure):
 
 class NicnesError(RuntimeError):
     pass
+
+
+class DecodeFault(NicnesError):
+    """NICNES_ERR_FAULT: a decode lost rows (coop hand-off or logit-slot timeout); the iteration's fitness is
+    NaN and its optimizer step was skipped on every rank, so theta / m / v are those before it.
+    Engine.clear_faults() makes the handle usable again."""
 
 
 _libs = {}
@@ -92,6 +98,8 @@ def lib(path=None):
         'nicnes_comm_init': (c.c_int, [vp, i32, i32, vp]),
         'nicnes_comm_attach': (c.c_int, [vp, vp]),
         'nicnes_comm_destroy': (c.c_int, [vp]),
+        'nicnes_comm_count': (c.c_int, [vp, vp, vp]),
+        'nicnes_clear_faults': (c.c_int, [vp, vp]),
         'nicnes_allgather_fitness': (c.c_int, [vp, vp, i32, vp, vp]),
         'nicnes_allreduce_grad': (c.c_int, [vp, vp, vp]),
         'nicnes_last_ratio': (c.c_int, [vp, vp, vp]),
@@ -112,4 +120,5 @@ def check(rc, handle=None, what=''):
         if handle:
             raw = lib().nicnes_last_error(handle)
             msg = raw.decode() if raw else ''
-        raise NicnesError('%s failed: %s%s' % (what, _NAMES.get(rc, 'error %d' % rc), (': ' + msg) if msg else ''))
+        cls = DecodeFault if rc == ERR_FAULT else NicnesError
+        raise cls('%s failed: %s%s' % (what, _NAMES.get(rc, 'error %d' % rc), (': ' + msg) if msg else ''))

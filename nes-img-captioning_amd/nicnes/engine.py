@@ -410,6 +410,12 @@ class Engine:
         check(self.L.nicnes_comm_destroy(self.h), self.h, 'comm_destroy')
         self.comm_ranks = 1
 
+    def comm_count(self):
+        """(ranks, this rank) as RCCL reports them for the bound communicator ((1, 0) with none)."""
+        n, r = ctypes.c_int32(), ctypes.c_int32()
+        check(self.L.nicnes_comm_count(self.h, ctypes.byref(n), ctypes.byref(r)), self.h, 'comm_count')
+        return int(n.value), int(r.value)
+
     def allgather_fitness(self, fit_local, fit_all):
         """fit_all [P_local * nranks, 2] <- every rank's fit_local [P_local, 2] (rank order)."""
         with torch.cuda.device(self.device):
@@ -422,6 +428,14 @@ class Engine:
         with torch.cuda.device(self.device):
             check(self.L.nicnes_allreduce_grad(self.h, _ptr(gsum), self._stream()), self.h, 'allreduce_grad')
         return gsum
+
+    def clear_faults(self):
+        """Clear a contained decode fault (nicnes_clear_faults): returns the fault counters it found
+        {'coop_timeouts', 'sample_slot_timeouts'}; the handle evaluates again afterwards."""
+        out = (ctypes.c_int64 * 2)()
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_clear_faults(self.h, out), self.h, 'clear_faults')
+        return {'coop_timeouts': int(out[0]), 'sample_slot_timeouts': int(out[1])}
 
     def stats(self):
         out = (ctypes.c_int64 * 4)()

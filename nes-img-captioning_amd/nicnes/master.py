@@ -87,6 +87,7 @@ class EngineMaster:
             engine.set_theta(theta)
         self.opt = make_optimizer(engine, spec)
         self.stats = []
+        self.faults = []
         self._batch_key = None
         self._n_batches = 1
         self.mutator = None
@@ -164,11 +165,42 @@ class EngineMaster:
             yield b
 
     # ------------------------------------------------------------------------ loops ------------
-    def run(self, batches, max_iterations=None):
+    def _iterate(self, runner, P):
+        """One iteration on the current batch: evaluate this rank's shard, exchange, noise sum, update."""
+        runner.evaluate(self.sched.iteration, n_batches=self._n_batches)
+        fit = runner.exchange_fitness()
+        _, w = self.e.rank_weights(fit)
+        self.e.grad_partial(self.sched.iteration, runner.m0, runner.local,
+                            w[runner.m0:runner.m0 + runner.local], self.sched.noise_stdev, out=runner.gsum)
+        runner.reduce_noise_sum()
+        return fit, self._update(runner.gsum, P)
+
+    def _record_fault(self, err, attempt, counters):
+        rec = {'iter': self.sched.iteration, 'attempt': attempt, 'error': str(err), **counters,
+               'time': time.time()}
+        self.faults.append(rec)
+        if self.rank == 0:
+            d = os.path.join(self.log_dir, 'faults')
+            os.makedirs(d, exist_ok=True)
+            with open(os.path.join(d, 'fault_i%d_a%d.json' % (self.sched.iteration, attempt)), 'w') as f:
+                json.dump(rec, f)
+        return rec
+
+    def run(self, batches, max_iterations=None, fault_retries=1):
         """Single-node loop: every rank evaluates its shard of the population; one all-gather of the
         fitness and one all-reduce of the noise sum per iteration (population.py). `batches`: a loader
         (batches drawn at the scheduled batch size) or an iterable of batches, re-iterated per epoch;
-        an iterable that yields nothing ends the run."""
+        an iterable that yields nothing ends the run.
+
+        Contained decode faults (nicnes.DecodeFault: a coop hand-off or logit-slot timeout) cost no state:
+        the faulted iteration's fitness is NaN on every rank and its optimizer step is skipped everywhere,
+        so theta / m / v / t are those before it. The iteration is recorded (self.faults, and
+        <log_dir>/faults/ on rank 0), the handle's fault counters cleared, and the same iteration (same
+        members, noise indices and batch) re-run, up to `fault_retries` times; after that a snapshot of
+        the pre-fault state is written (rank 0) and the DecodeFault propagates, so the process exits
+        non-zero with a resumable snapshot instead of a half-finished run. The reference has no such
+        path: a dead worker process is restarted and the master waits (main.py:107-141)."""
+        from ._lib import DecodeFault
         P = self.spec.nb_offspring
         max_it = max_iterations or self.spec.config.max_nb_iterations
         runner = None
@@ -184,13 +216,16 @@ class EngineMaster:
                 if runner is None or runner.sigma != self.sched.noise_stdev:
                     runner = PopulationRunner(self.e, P, self.sched.noise_stdev, rank=self.rank,
                                               world_size=self.world, group=self.group, comm=self.comm)
-                runner.evaluate(self.sched.iteration, n_batches=self._n_batches)
-                fit = runner.exchange_fitness()
-                _, w = self.e.rank_weights(fit)
-                self.e.grad_partial(self.sched.iteration, runner.m0, runner.local,
-                                    w[runner.m0:runner.m0 + runner.local], self.sched.noise_stdev, out=runner.gsum)
-                runner.reduce_noise_sum()
-                ratio = self._update(runner.gsum, P)
+                for attempt in range(int(fault_retries) + 1):
+                    try:
+                        fit, ratio = self._iterate(runner, P)
+                        break
+                    except DecodeFault as err:
+                        self._record_fault(err, attempt, self.e.clear_faults())
+                        if attempt == int(fault_retries):
+                            if self.rank == 0:
+                                self.save_snapshot()
+                            raise
                 self._record(fit, ratio, t0)
                 self._after_update()
                 self._maybe_snapshot()

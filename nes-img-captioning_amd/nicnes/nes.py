@@ -113,6 +113,11 @@ class EnginePolicy:
         self.spec = spec
         self.shapes = param_shapes(engine)
         self._batch_key = None
+        # the eval rollouts' draw stream (sampled modes): a per-process random start, so two workers sharing
+        # --noise_seed, or a restarted worker, do not replay each other's draws -- each reference worker process
+        # draws from its own unseeded RandomState (nic_nes_worker.py:22). The engine hashes the low 32 bits.
+        self._eval_salt = int.from_bytes(os.urandom(4), 'little')
+        self._eval_calls = 0
         if spec is not None:
             engine.set_fitness_mode(spec.fitness)      # CaptPolicy's Fitness (policies.py:22-61)
 
@@ -178,6 +183,10 @@ class EnginePolicy:
             self._batch_rows = rows
         return self._batch_rows
 
+    def eval_iteration(self):
+        """The draw-stream index of the newest eval rollout: this process's salt + its call count (mod 2^32)."""
+        return (self._eval_salt + self._eval_calls) & 0xffffffff
+
     def rollout(self, placeholder, data, config):
         """CaptPolicy.rollout (policies.py:86-128) of the current theta: float(100 * mean CIDEr-D) for
         'greedy' and 'sample', 100 * the mean self-critical difference for 'self_critical', the criterion
@@ -186,8 +195,8 @@ class EnginePolicy:
         # theta itself, decoded once (nicnes_evaluate_theta: the two antithetic signs split the images);
         # with several batches held, member 0's batch (member_batches' rule)
         # the sampled modes draw afresh per eval rollout, as the reference's worker RNG does
-        self._eval_calls = getattr(self, '_eval_calls', 0) + 1
-        fit = self.e.evaluate_theta(0, iteration=self._eval_calls)
+        self._eval_calls += 1
+        fit = self.e.evaluate_theta(0, iteration=self.eval_iteration())
         return float(fit[0].item())
 
 

@@ -91,8 +91,11 @@ def _factory(path):
     return getattr(importlib.import_module(mod), fn)
 
 
-def worker_main(index, device, args):
-    """One worker process: engine on `device`, then the serve loop until the stop key is set."""
+def worker_main(index, device, args, shared_device=False):
+    """One worker process: engine on `device`, then the serve loop until the stop key is set.
+    shared_device: another worker of this pool runs on the same GPU. The coop decode then stays off: its
+    workgroups wait for each other and assume the whole device, which a second process's kernels break
+    (a stalled hand-off is a contained fault, but every later evaluate of the worker then fails)."""
     logging.basicConfig(format='[%(asctime)s pid=%(process)d] %(message)s', level=logging.INFO)
     from nicnes import config as C
     from nicnes import transport as T
@@ -105,6 +108,8 @@ def worker_main(index, device, args):
     exp = client.get_experiment()
     spec = C.ExperimentSpec(exp, vocab_size=args.vocab_size)
     engine, worker = _factory(args.engine_factory)(spec, args, device)
+    if shared_device and hasattr(engine, 'set_decode_coop'):
+        engine.set_decode_coop(0)
     stop = threading.Event()
 
     def watch():
@@ -175,7 +180,8 @@ def supervise(args):
     store = T.connect(cfg[0] if isinstance(cfg, tuple) else cfg)
 
     def start(i):
-        p = ctx.Process(target=worker_main, args=(i, devices[i], args), name='nicnes-worker-%d' % i)
+        shared = devices[:n].count(devices[i]) > 1
+        p = ctx.Process(target=worker_main, args=(i, devices[i], args, shared), name='nicnes-worker-%d' % i)
         p.start()
         return p
 

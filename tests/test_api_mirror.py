@@ -506,4 +506,71 @@ def test_eval_rollouts_draw_a_fresh_stream_each(workload):
     data = {'fc_feats': np.repeat(workload[2], 5, axis=0), 'gts': workload[3]}
     pol.rollout(None, data, None)
     pol.rollout(None, data, None)
-    assert seen == [1, 2]
+    s0 = pol._eval_salt
+    assert seen == [(s0 + 1) & 0xffffffff, (s0 + 2) & 0xffffffff]     # this process's salt + the call count
+
+
+class _FaultingEngine(OracleEngine):
+    """The oracle engine with the HIP engine's contained-fault contract: the first `faults` optimizer steps
+    raise DecodeFault and change nothing (the device skips them); clear_faults reports and clears."""
+
+    def __init__(self, *a, faults=1, **k):
+        super().__init__(*a, **k)
+        self.faults_left, self.cleared = faults, 0
+
+    def adam_step(self, *a, **k):
+        if self.faults_left > 0:
+            self.faults_left -= 1
+            from nicnes import DecodeFault
+            raise DecodeFault('adam_step failed: contained decode fault: coop decode: hand-off timeout')
+        return super().adam_step(*a, **k)
+
+    def clear_faults(self):
+        self.cleared += 1
+        return {'coop_timeouts': 1, 'sample_slot_timeouts': 0}
+
+
+def test_master_reruns_a_contained_fault(workload, tmp_path):
+    """EngineMaster.run: a faulted iteration is recorded, the handle cleared and the same
+    iteration re-run, ending as the unfaulted run; past fault_retries a snapshot is written and the fault raised."""
+    import nicnes
+    dims, theta, fc, gts, df, n, table = workload
+    P = 4
+    ref_e = OracleEngine(dims, theta, fc, gts, df, n, table)
+    ref = M.EngineMaster(_spec(P), ref_e, log_dir=str(tmp_path / 'ref'))
+    ref.run([(fc, gts)] * 3, max_iterations=3)
+    e = _FaultingEngine(dims, theta, fc, gts, df, n, table, faults=1)
+    m = M.EngineMaster(_spec(P), e, log_dir=str(tmp_path / 'f1'))
+    m.run([(fc, gts)] * 3, max_iterations=3, fault_retries=1)
+    assert e.cleared == 1 and [(f['iter'], f['attempt']) for f in m.faults] == [(1, 0)]
+    assert (tmp_path / 'f1' / 'faults' / 'fault_i1_a0.json').exists()
+    assert [s['score_mean'] for s in m.stats] == [s['score_mean'] for s in ref.stats]
+    assert np.array_equal(e.adam.theta, ref_e.adam.theta)
+    e2 = _FaultingEngine(dims, theta, fc, gts, df, n, table, faults=2)
+    m2 = M.EngineMaster(_spec(P), e2, log_dir=str(tmp_path / 'f2'))
+    with pytest.raises(nicnes.DecodeFault):
+        m2.run([(fc, gts)] * 3, max_iterations=3, fault_retries=1)
+    assert [(f['iter'], f['attempt']) for f in m2.faults] == [(1, 0), (1, 1)] and m2.stats == []
+    assert list((tmp_path / 'f2' / 'snapshot').glob('z_info_e1_i1-0.json'))
+
+
+def test_eval_rollout_draw_streams_differ_between_processes(workload):
+    """two workers sharing --noise_seed (or a restarted worker) must not replay each other's eval
+    draws. Each EnginePolicy starts its eval stream at a random 32-bit salt (the engine hashes the low 32 bits
+    of the iteration), then steps by one per rollout."""
+    dims, theta, fc, gts, df, n, table = workload
+    seen = []
+
+    class _Rec(OracleEngine):
+        def evaluate_theta(self, batch=0, iteration=0):
+            seen.append(iteration)
+            return super().evaluate_theta(batch, iteration)
+
+    pa = N.EnginePolicy(_Rec(dims, theta, fc, gts, df, n, table))
+    pb = N.EnginePolicy(_Rec(dims, theta, fc, gts, df, n, table))
+    batch = {'fc_feats': np.repeat(fc, 5, axis=0), 'gts': gts}
+    for p in (pa, pb, pa):
+        p.rollout(None, batch, None)
+    assert seen[0] != seen[1]                               # two processes' first eval draws
+    assert seen[2] == (seen[0] + 1) & 0xffffffff            # the next rollout of the same process
+    assert all(0 <= s < 2 ** 32 for s in seen)

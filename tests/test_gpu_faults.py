@@ -12,6 +12,7 @@ sampled decode fewer logit slots than it has workgroups.
 Also here: the coop grid is bounded by the occupancy query (the split path takes larger grids),
 and nicnes_evaluate_theta writes exactly its rows_total x T outputs at odd batch sizes."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -168,3 +169,80 @@ def test_eval_theta_writes_exactly_its_rows(B):
         assert torch.equal(seq[:B], ref_seq) and torch.equal(lp[:B], ref_lp) and torch.equal(fit, ref_fit)
     finally:
         e.close()
+
+
+def _master_spec(P):
+    from nicnes import config as C
+    exp = {'algorithm': 'nic_nes', 'nb_offspring': P,
+           'config': {'noise_stdev': 0.01, 'batch_size': 128, 'l2coeff': 1e-3, 'snapshot_freq': 0, 'single_batch': True},
+           'policy_options': {'net': 'fc_caption', 'fitness': 'greedy', 'model_options': {}},
+           'optimizer_options': {'type': 'adam', 'args': {'stepsize': 1e-2}}}
+    return C.ExperimentSpec(exp)
+
+
+def _master_run(monkeypatch, tmp_path, stall_launches, iterations=2, retries=1):
+    """EngineMaster.run on the coop path (P = 4 members, S = 4) with the first `stall_launches` coop launches
+    stalled past the spin bound (0: no fault). Returns (master, engine); the caller closes the engine."""
+    import nicnes
+    from nicnes import master as M
+    if stall_launches:
+        monkeypatch.setenv('NICNES_TEST_COOP_STALL', '700')
+        monkeypatch.setenv('NICNES_TEST_COOP_STALL_LAUNCHES', str(stall_launches))
+    e = _engine()
+    monkeypatch.delenv('NICNES_TEST_COOP_STALL', raising=False)
+    monkeypatch.delenv('NICNES_TEST_COOP_STALL_LAUNCHES', raising=False)
+    _load(e, 128)
+    e.set_decode_split(4, 4)
+    assert e.decode_path(128, 4) == 'coop'
+    fc = np.random.Generator(np.random.PCG64(3)).standard_normal((128, 2048)).astype(np.float32)
+    gts = [np.asarray([[(7 * b + k) % 60 + 1 for k in range(8)] + [0] * 8], np.int32) for b in range(128)]
+    m = M.EngineMaster(_master_spec(4), e, log_dir=str(tmp_path), theta=e.theta()[1].cpu().numpy())
+    try:
+        m.run([(fc, gts)] * iterations, max_iterations=iterations, fault_retries=retries)
+    except Exception:
+        e.close()
+        raise
+    return m, e
+
+
+def test_master_reruns_a_faulted_iteration(monkeypatch, tmp_path):
+    """one coop hand-off timeout in iteration 1 is recorded, the handle's fault cleared and the
+    iteration re-run; the run then ends exactly as an unfaulted run (theta, m, v, t, fitness bit for bit)."""
+    import json
+    import os
+    ref, e0 = _master_run(monkeypatch, tmp_path / 'clean', 0)
+    try:
+        got, e1 = _master_run(monkeypatch, tmp_path / 'faulted', 1)
+        try:
+            assert ref.faults == [] and len(got.faults) == 1
+            f = got.faults[0]
+            assert f['iter'] == 1 and f['attempt'] == 0 and f['coop_timeouts'] > 0 and 'hand-off' in f['error']
+            assert os.path.exists(tmp_path / 'faulted' / 'faults' / 'fault_i1_a0.json')
+            with open(tmp_path / 'faulted' / 'faults' / 'fault_i1_a0.json') as fh:
+                assert json.load(fh)['iter'] == 1
+            assert [s['score_mean'] for s in got.stats] == [s['score_mean'] for s in ref.stats]
+            assert [s['update_ratio'] for s in got.stats] == [s['update_ratio'] for s in ref.stats]
+            for a, b in zip(e1.adam_state()[:2] + e1.theta(), e0.adam_state()[:2] + e0.theta()):
+                assert torch.equal(a, b)
+            assert e1.adam_state()[2] == e0.adam_state()[2] == 2
+            assert e1.stats()['coop_timeouts'] == 0                 # cleared
+        finally:
+            e1.close()
+    finally:
+        e0.close()
+
+
+def test_master_gives_up_after_the_retries_with_a_snapshot(monkeypatch, tmp_path):
+    """Two faulted tries of iteration 1 with fault_retries=1: DecodeFault propagates (the process would exit
+    non-zero), both tries are recorded, theta / m / v / t are the initial ones and a resumable snapshot exists."""
+    import glob
+    import nicnes
+    with pytest.raises(nicnes.DecodeFault):
+        _master_run(monkeypatch, tmp_path, 2, iterations=1, retries=1)
+    assert sorted(os.path.basename(p) for p in glob.glob(str(tmp_path / 'faults' / '*.json'))) == \
+        ['fault_i1_a0.json', 'fault_i1_a1.json']
+    assert glob.glob(str(tmp_path / 'snapshot' / 'z_info_e*_i1-0.json'))
+    assert os.path.exists(tmp_path / 'snapshot' / 'optimizer.tar')
+    from nicnes import nes as N
+    st = N._load_state(str(tmp_path / 'snapshot' / 'optimizer.tar'))
+    assert st['t'] == 0 and not np.any(st['m'])

@@ -326,6 +326,48 @@ def test_stage_scan_pick_equals_the_full_walk(eng, monkeypatch, gain):
     assert r1 == 0 and r2 == 0, (r1, r2)
 
 
+@pytest.mark.parametrize('gain', [1.0, 4.0])
+def test_stage_scan_pick_equals_the_full_walk_at_scale(gain):
+    """The same pick-vs-walk identity on a workload where a 4e-5 mis-pick rate cannot hide:
+    P = 64 members x 2 signs x 640 rows (128 images x 5 sampled copies) x 16 steps = 1.31 M draws from the
+    engine's own counter-based stream, in one launch per engine. Round 4's store-data hazard (the block sums
+    zeroed under their own 16-byte store) put ~450 of 10.5 M picks one stage late: ~55 expected here."""
+    import nicnes
+    dims = O.Dims()
+    theta = O.make_theta(dims, 5, gain, 0.1 if gain > 1 else 0.0)
+    B, P = 128, 64
+    fc = np.random.Generator(np.random.PCG64(81)).standard_normal((B, dims.F)).astype(np.float32)
+    table = O.noise_table(NOISE_LEN, 123)
+    gts = [np.asarray([[(7 * b + k) % 60 + 1 for k in range(8)] + [0] * 8], np.int32) for b in range(B)]
+    keys, vals = nicnes.df_table_arrays({})
+    out = []
+    for exact in ('0', '1'):
+        import os
+        os.environ['NICNES_FORCE_EXACT'] = exact
+        try:
+            e = nicnes.Engine(max_batch=B, max_members=P, noise_len=NOISE_LEN, noise_seed=7)
+        finally:
+            os.environ.pop('NICNES_FORCE_EXACT', None)
+        try:
+            e.set_noise_table(table)
+            e.set_theta(theta)
+            e.set_df_table(keys, vals, np.log(4096.0))
+            e.set_batch(fc, gts)
+            e.set_fitness_mode('sample')
+            e.set_rows_per_image(5)
+            _, seq, lp = e.evaluate(3, 0, P, SIGMA, return_seq=True, return_lp=True)
+            st = e.stats()
+            out.append((seq.cpu().numpy(), lp.cpu().numpy(), st['sample_stage_fallbacks'], st['sample_slot_timeouts']))
+        finally:
+            e.close()
+    (s1, l1, r1, t1), (s2, l2, r2, t2) = out
+    assert s1.shape == (P, 2, 5 * B, dims.T)
+    assert t1 == t2 == 0 and r1 == 0 and r2 == 0, (r1, r2, t1, t2)
+    bad = int((s1 != s2).any(axis=-1).sum())
+    assert bad == 0, '%d of %d rows picked differently from the full walk' % (bad, P * 2 * 5 * B)
+    assert np.array_equal(l1.view(np.int32), l2.view(np.int32))
+
+
 def test_logit_slots_are_reused_across_workgroups():
     """More sampled workgroups than logit slots (300 members x 1 slab against n_CU + 16 slots): workgroups that
     start after others finished reuse their slots. Every member's tokens and log-probs equal the same member
