@@ -386,7 +386,7 @@ def main():
         def prepare(it_):
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
-            mutator.prepare(it_, eng.theta()[1], fc_rows)       # SM-G-SUM: enqueued on the engine's stream
+            mutator.prepare(it_, lambda: eng.theta()[1], fc_rows)   # SM-G-SUM: enqueued on the engine's stream
             ev1.record()
             mut_s.append((ev0, ev1))
     else:

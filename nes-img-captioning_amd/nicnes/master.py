@@ -101,7 +101,7 @@ class EngineMaster:
         (nicnes.mutations)."""
         if self.mutator is not None and self.mutator.active:
             from .mutations import batch_fc
-            self.mutator.prepare(self.sched.iteration, self.e.theta()[1], batch_fc(batch))
+            self.mutator.prepare(self.sched.iteration, lambda: self.e.theta()[1], batch_fc(batch))
 
     # ------------------------------------------------------------------------ helpers ----------
     def _set_batch(self, batch):

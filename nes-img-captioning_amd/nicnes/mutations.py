@@ -93,9 +93,13 @@ class Mutator:
         return self.mode in ('SM-G-SUM', 'SM-PROPORTIONAL')
 
     def prepare(self, key, theta32, fc_unique):
+        """theta32: the fp32 theta, or a callable returning it (read only by SM-PROPORTIONAL: SM-G-SUM takes theta
+        from the engine itself, so the callers pass `lambda: engine.theta()[1]` and no copy is made for it)."""
         if not self.active or key == self._key:
             return self.vector
         if self.mode == 'SM-PROPORTIONAL':
+            if callable(theta32):
+                theta32 = theta32()
             th = theta32.detach().cpu().numpy() if isinstance(theta32, torch.Tensor) else np.asarray(theta32)
             self.vector = proportional_vector(th.astype(np.float32, copy=False))
             self.e.set_mutation('scale', self.vector)

@@ -229,7 +229,8 @@ class EngineWorker:
         if self.mutator is not None and self.mutator.active:
             # calc_sensitivity of the task's theta on its batch before evolve (nic_nes_worker.py:137-142)
             from .mutations import batch_fc
-            self.mutator.prepare((task_id, getattr(self, '_cur_version', 0)), self.e.theta()[1], batch_fc(task_data.batch_data))
+            self.mutator.prepare((task_id, getattr(self, '_cur_version', 0)), lambda: self.e.theta()[1],
+                                 batch_fc(task_data.batch_data))
 
     def fitness_batch(self, task_id, task_data, member_begin, count, batches=None):
         """-> list of NESResult(fitness=[f+, f-] fp64, noise_idx, member). batches (single_batch: false on the
