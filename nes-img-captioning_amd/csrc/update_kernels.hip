@@ -76,6 +76,46 @@ __global__ __launch_bounds__(1024) void nicnes_rank_sort_kernel(const double* fi
     }
 }
 
+// n <= RANK_CHUNK (every population up to 1024 members): no sort. Workgroup g holds all n keys in LDS and ranks
+// its 32 entries (16 members): 8 groups of 32 lanes count the pairs below each entry over an eighth of the keys
+// each, then the counts are added. The same stable rank as the two passes below, in one launch of n / 32
+// workgroups (round 5: the sort pass and the search pass took 29.5 us per iteration at P = 64, 31 at P = 512)
+#define RANK_SMALL_E 32
+#define RANK_SMALL_G (256 / RANK_SMALL_E)
+__global__ __launch_bounds__(256) void nicnes_rank_small_kernel(const double* fit, int n, double* cr_out, float* w_out) {
+    __shared__ uint64_t k[RANK_CHUNK];
+    __shared__ int cnt[RANK_SMALL_G][RANK_SMALL_E];
+    __shared__ double cr[RANK_SMALL_E];
+    for (int e = threadIdx.x; e < n; e += blockDim.x) k[e] = rank_key(fit[e]);
+    __syncthreads();
+    const int l = threadIdx.x % RANK_SMALL_E, g = threadIdx.x / RANK_SMALL_E;
+    const int e = blockIdx.x * RANK_SMALL_E + l;
+    if (e < n) {
+        const uint64_t ke = k[e];
+        const int j0 = g * n / RANK_SMALL_G, j1 = (g + 1) * n / RANK_SMALL_G;
+        int r = 0;
+#pragma unroll 4
+        for (int j = j0; j < j1; ++j)             // every lane of the group reads the same key: an LDS broadcast
+            r += pair_less(k[j], (uint32_t)j, ke, (uint32_t)e) ? 1 : 0;
+        cnt[g][l] = r;
+    }
+    __syncthreads();
+    if (g == 0 && e < n) {
+        int r = 0;
+#pragma unroll
+        for (int q = 0; q < RANK_SMALL_G; ++q) r += cnt[q][l];
+        double y = (double)r;
+        y /= (double)(n - 1);                      // y /= (x.size - 1)   (compute_centered_ranks)
+        y -= 0.5;                                  // y -= .5
+        cr[l] = y;
+        if (cr_out) cr_out[e] = y;
+    }
+    __syncthreads();
+    const int pl = threadIdx.x, p = blockIdx.x * (RANK_SMALL_E / 2) + pl;
+    if (pl < RANK_SMALL_E / 2 && 2 * p < n)
+        w_out[p] = (float)(cr[2 * pl] - cr[2 * pl + 1]);   // cr[:, 0] - cr[:, 1], then fp32 (gradient_estimate)
+}
+
 __device__ __forceinline__ int chunk_lower_bound(const uint64_t* key, const uint32_t* idx, uint64_t kq, uint32_t iq) {
     int lo = 0, hi = RANK_CHUNK;
     while (lo < hi) {
@@ -168,9 +208,56 @@ __global__ __launch_bounds__(256) void nicnes_grad_kernel(const float* __restric
 // one Adam step; partial sums of step^2 and theta_old^2 per block for the update ratio.
 // No-op (theta, m, v untouched; ratio NaN) after a faulted decode: this handle's counters (p.fault), or a NaN
 // first entry of the noise sum, which a faulted rank's nicnes_grad_kernel writes and the all-reduce spreads
+__device__ __forceinline__ void adam_one(const AdamParams& p, int64_t j, double& s2, double& t2) {
+    const double th = p.theta64[j];
+    // globalg g' = -g + l2coeff * theta (nic_nes_master.py:311-318), or given directly
+    // (Optimizer.update(globalg)). Before the first update theta, and so g', are fp32 arrays.
+    float gp32 = 0.f;
+    double gp64;
+    if (p.globalg) {
+        gp64 = p.globalg[j];
+        gp32 = (float)gp64;
+    } else {
+        const float g = p.gsum[j] / p.two_f;             // gradient_est /= ranked_fitnesses.size (fp32)
+        if (p.theta_is_fp32) {
+            gp32 = -g + p.l2coeff32 * (float)th;
+            gp64 = gp32;
+        } else {
+            gp64 = (double)(-g) + p.l2coeff * th;
+        }
+    }
+    // numpy keeps python_float * fp32_array in fp32 (NEP 50): at the first update the
+    // (1 - b) * g' products are fp32, added to the fp64 state (optimizers.py:45,81-82)
+    double step;
+    if (p.kind == 0) {                                   // Adam._compute_step, optimizers.py:78-83
+        double m, v;
+        if (p.g_is_fp32) {
+            m = p.beta1 * p.m[j] + (double)(p.one_minus_beta1_32 * gp32);
+            v = p.beta2 * p.v[j] + (double)(p.one_minus_beta2_32 * (gp32 * gp32));
+        } else {
+            m = p.beta1 * p.m[j] + p.one_minus_beta1 * gp64;
+            v = p.beta2 * p.v[j] + p.one_minus_beta2 * (gp64 * gp64);
+        }
+        step = (-p.a * m) / (sqrt(v) + p.epsilon);
+        p.m[j] = m;
+        p.v[j] = v;
+    } else {                                             // SGD._compute_step, optimizers.py:44-47
+        const double v = p.g_is_fp32 ? p.beta1 * p.v[j] + (double)(p.one_minus_beta1_32 * gp32)
+                                         : p.beta1 * p.v[j] + p.one_minus_beta1 * gp64;
+        step = p.neg_stepsize * v;
+        p.v[j] = v;
+    }
+    const double nt = th + step;
+    p.theta64[j] = nt;
+    p.theta32[j] = (float)nt;
+    s2 += step * step;
+    t2 += th * th;
+}
+
+// grid-stride over the parameters (ADAM_BLOCKS workgroups, so the fixed-order sum of the partials below reads
+// 2 x ADAM_BLOCKS doubles instead of 2 x D / 256: 13 us of one workgroup's dependent loads at D = 2.87 M)
 __global__ __launch_bounds__(256) void nicnes_adam_kernel(AdamParams p) {
     __shared__ double red[2][256];
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double s2 = 0.0, t2 = 0.0;
     const bool skip = decode_fault(p.fault) || (p.gsum != nullptr && p.gsum[0] != p.gsum[0]);
     // the explicit skip flag beside the norms (norms[2]): the host raises the fault error only when it is set,
@@ -178,50 +265,9 @@ __global__ __launch_bounds__(256) void nicnes_adam_kernel(AdamParams p) {
     if (blockIdx.x == 0 && threadIdx.x == 0) p.skip_out[0] = skip ? 1.0 : 0.0;
     if (skip) {
         s2 = t2 = __builtin_nan("");
-    } else if (j < p.dim) {
-        const double th = p.theta64[j];
-        // globalg g' = -g + l2coeff * theta (nic_nes_master.py:311-318), or given directly
-        // (Optimizer.update(globalg)). Before the first update theta, and so g', are fp32 arrays.
-        float gp32 = 0.f;
-        double gp64;
-        if (p.globalg) {
-            gp64 = p.globalg[j];
-            gp32 = (float)gp64;
-        } else {
-            const float g = p.gsum[j] / p.two_f;             // gradient_est /= ranked_fitnesses.size (fp32)
-            if (p.theta_is_fp32) {
-                gp32 = -g + p.l2coeff32 * (float)th;
-                gp64 = gp32;
-            } else {
-                gp64 = (double)(-g) + p.l2coeff * th;
-            }
-        }
-        // numpy keeps python_float * fp32_array in fp32 (NEP 50): at the first update the
-        // (1 - b) * g' products are fp32, added to the fp64 state (optimizers.py:45,81-82)
-        double step;
-        if (p.kind == 0) {                                   // Adam._compute_step, optimizers.py:78-83
-            double m, v;
-            if (p.g_is_fp32) {
-                m = p.beta1 * p.m[j] + (double)(p.one_minus_beta1_32 * gp32);
-                v = p.beta2 * p.v[j] + (double)(p.one_minus_beta2_32 * (gp32 * gp32));
-            } else {
-                m = p.beta1 * p.m[j] + p.one_minus_beta1 * gp64;
-                v = p.beta2 * p.v[j] + p.one_minus_beta2 * (gp64 * gp64);
-            }
-            step = (-p.a * m) / (sqrt(v) + p.epsilon);
-            p.m[j] = m;
-            p.v[j] = v;
-        } else {                                             // SGD._compute_step, optimizers.py:44-47
-            const double v = p.g_is_fp32 ? p.beta1 * p.v[j] + (double)(p.one_minus_beta1_32 * gp32)
-                                             : p.beta1 * p.v[j] + p.one_minus_beta1 * gp64;
-            step = p.neg_stepsize * v;
-            p.v[j] = v;
-        }
-        const double nt = th + step;
-        p.theta64[j] = nt;
-        p.theta32[j] = (float)nt;
-        s2 = step * step;
-        t2 = th * th;
+    } else {
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < p.dim; j += stride) adam_one(p, j, s2, t2);
     }
     red[0][threadIdx.x] = s2;
     red[1][threadIdx.x] = t2;
@@ -299,6 +345,11 @@ extern "C" size_t nicnes_rank_scratch_pairs(int n) { return (size_t)((n + RANK_C
 
 extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, uint64_t* skey, uint32_t* sidx, double* cr_out,
                                          float* w_out, hipStream_t s) {
+    if (n <= RANK_CHUNK) {
+        hipLaunchKernelGGL(nicnes_rank_small_kernel, dim3((n + RANK_SMALL_E - 1) / RANK_SMALL_E), dim3(256), 0, s, fit, n,
+                           cr_out, w_out);
+        return hipGetLastError();
+    }
     const int nchunks = (n + RANK_CHUNK - 1) / RANK_CHUNK;
     hipLaunchKernelGGL(nicnes_rank_sort_kernel, dim3(nchunks), dim3(RANK_CHUNK / 2), 0, s, fit, n, skey, sidx);
     hipLaunchKernelGGL(nicnes_rank_kernel, dim3((n / 2 + 255) / 256), dim3(256), 0, s, fit, n, skey, sidx, cr_out, w_out);
@@ -411,7 +462,8 @@ extern "C" hipError_t nicnes_launch_iota_stride(uint64_t* out, int n, uint64_t s
     return hipGetLastError();
 }
 
-extern "C" int nicnes_adam_blocks(int64_t dim) { return (int)((dim + 255) / 256); }
+#define ADAM_BLOCKS 2048
+extern "C" int nicnes_adam_blocks(int64_t dim) { return (int)std::min<int64_t>((dim + 255) / 256, ADAM_BLOCKS); }
 
 extern "C" hipError_t nicnes_launch_adam(const AdamParams* p, double* norms_out, hipStream_t s) {
     const int nb = nicnes_adam_blocks(p->dim);

@@ -414,13 +414,16 @@ def test_bounded_lse_undecided_rows_take_the_exact_pass(monkeypatch, shape):
         e.close()
 
 
-@pytest.mark.parametrize('P', [2048, 8192, 1000], ids=['P2048', 'P8192', 'P1000_partial_chunk'])
+@pytest.mark.parametrize('P', [2048, 8192, 1000, 1024, 1025, 64, 1],
+                         ids=['P2048', 'P8192', 'P1000', 'P1024_small_max', 'P1025_sort', 'P64', 'P1'])
 def test_rank_weights_bit_exact_large(eng, P):
-    """The sort-based rank (chunk bitonic sort + lower bounds) at configs[3]'s pop=2048 and beyond the
-    old one-workgroup cap; many ties, -0.0 / +0.0 and NaN (last, as numpy's argsort places it)."""
+    """Both rank paths: the one-launch count (2P <= 2048 entries: the bench's P = 512 and its 64 / 128 per GPU)
+    and the sort-based rank (chunk bitonic sort + lower bounds) at configs[3]'s pop=2048 and beyond; the boundary
+    on either side; many ties, -0.0 / +0.0 and NaN (last, as numpy's argsort places it)."""
     rng = np.random.default_rng(P)
     fit = np.round(rng.random((P, 2)) * 200) / 4.0
-    fit[3, 0], fit[5, 1], fit[7, 0] = -0.0, 0.0, np.nan
+    if P >= 8:
+        fit[3, 0], fit[5, 1], fit[7, 0] = -0.0, 0.0, np.nan
     cr, w = eng.rank_weights(torch.from_numpy(fit).cuda())
     w_ref, cr_ref = O.weights_from_fitness(fit)
     assert np.array_equal(cr.cpu().numpy(), cr_ref)
