@@ -83,6 +83,10 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef CELL_MIDSTORE
 #define CELL_MIDSTORE 1    // the steps kernel's cell stores tile m + 1 mid-way through tile m's MFMAs (-0.3 %, greedy)
 #endif
+#ifndef LOGIT_PEEL
+#define LOGIT_PEEL 1       // logit stages: the last two stages peeled off the stage loop (round 5: greedy steps kernel
+                           // -0.55 %, B = 64 steps2 -4.1 %; not kept for the coop (+1.4 %) and sampled (+2.2 %) decodes)
+#endif
 #ifndef LOGIT_MID_AT
 #define LOGIT_MID_AT 6     // ... before half-chunk LOGIT_MID_AT of 8 (measured: 5-7 equal, 2 and 8 -0.8 %)
 #endif
@@ -1041,7 +1045,7 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
 
 // Measured and not kept (git history, r04): per-wave LDS progress words in place of the per-stage barrier (+0.4 %),
 // a chain-a-only last stage for the coop ranges (+1.3 % / +2.2 % at P = 64 / 128, or spills inside the loop).
-template <int G, bool PAIRS, class Tail = NoTail, class Hook = NoHook>
+template <int G, bool PAIRS, bool PEEL = (LOGIT_PEEL != 0), class Tail = NoTail, class Hook = NoHook>
 __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, uint64_t nidx, int wave, int sgn,
                                              int hf, const float (&hB)[64], int s0, int s1, RowState& st,
                                              Stage64Regs& s64, bool preloaded = false, Tail&& tail = Tail(),
@@ -1067,13 +1071,17 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
     // the registers carry stage s + 1 into stage s: its W+- tile is written before the last quarter of the
     // MFMAs of stage s (its buffer was last read in stage s - 1), then the loads of stage s + 2 are issued,
     // so the end of a stage has no staging wait and no LDS-write tail in front of the barrier
-    if (s0 + 1 < s1) stage64_load_o(lsrc(s0 + 1), lo, bias, s64);
+    if (PEEL) stage64_load_o(lsrc(min(s0 + 1, s1 - 1)), lo, bias, s64);   // (unconditional: one definition of s64)
+    else if (s0 + 1 < s1) stage64_load_o(lsrc(s0 + 1), lo, bias, s64);
 #endif
     __syncthreads();
     f32x16 a0, a1, b0, b1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { b0[r] = NEG_INF; b1[r] = NEG_INF; }
-    auto stage = [&](int s, f32x16& o0, f32x16& o1, const f32x16& q0, const f32x16& q1) {
+    // MODE (LOGIT_PEEL): 0 a stage with two more after it (store s + 1, load s + 2), 1 the last but one (store
+    // s + 1), 2 the last (the tail's loads); -1: decided at run time (the loop without the peel)
+    auto stage = [&](auto mode_t, int s, f32x16& o0, f32x16& o1, const f32x16& q0, const f32x16& q1) {
+        constexpr int MODE = decltype(mode_t)::value;
         const int sn = min(s + 1, s1 - 1);
 #if !LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
         stage64_load_o(lsrc(sn), lo, bias, s64);
@@ -1085,7 +1093,14 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
 #if LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
             // s64 is loaded on every non-last path (at s1 - 2 the load repeats tile s1 - 1): a conditional load
             // here would make the compiler copy the 32 staging registers at every stage to merge the paths
-            if (s + 1 < s1) {
+            if constexpr (MODE == 0) {
+                stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
+                stage64_load_o(lsrc(min(s + 2, s1 - 1)), lo, bias, s64);
+            } else if constexpr (MODE == 1) {
+                stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
+            } else if constexpr (MODE == 2) {
+                tail();
+            } else if (s + 1 < s1) {
                 stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
                 stage64_load_o(lsrc(min(s + 2, s1 - 1)), lo, bias, s64);
             } else {
@@ -1134,15 +1149,37 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
             epilogue32<PAIRS>(st, q0, 64 * s + vl);
         }
     };
+    if constexpr (PEEL) {
+    // the last two stages peeled off the loop: inside it every stage stores and loads unconditionally, so the
+    // staging registers have one definition and no copy (with a wait for their loads) at a merge point
+    using M0 = std::integral_constant<int, 0>;
+    using M1 = std::integral_constant<int, 1>;
+    using M2 = std::integral_constant<int, 2>;
+    int s = s0;
+    for (; s + 2 < s1; s += 2) {
+        stage(M0{}, s, a0, a1, b0, b1);
+        stage(M0{}, s + 1, b0, b1, a0, a1);
+    }
+    if (s + 1 == s1) {
+        stage(M2{}, s, a0, a1, b0, b1);
+        last(a0, a1, s);
+    } else {
+        stage(M1{}, s, a0, a1, b0, b1);
+        stage(M2{}, s + 1, b0, b1, a0, a1);
+        last(b0, b1, s + 1);
+    }
+    } else {
+    using MR = std::integral_constant<int, -1>;
     for (int s = s0; s < s1; s += 2) {
-        stage(s, a0, a1, b0, b1);
+        stage(MR{}, s, a0, a1, b0, b1);
         if (s + 1 == s1) {
             last(a0, a1, s);
             return;
         }
-        stage(s + 1, b0, b1, a0, a1);
+        stage(MR{}, s + 1, b0, b1, a0, a1);
     }
     last(b0, b1, s1 - 1);
+    }
 }
 
 // gate tiles of the cell: tile m = 0..19 is gate chunk tile_q(m) (order g1, g2, i, f, o) of the
@@ -1462,7 +1499,8 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
             const SampleStage ss{c.slog_r, 16u * (uint32_t)lane_fresh() + SLOG_WAVE_BYTES * (uint32_t)c.wave,
                                  16u * (uint32_t)lane_fresh() + 1024u * (uint32_t)c.wave, (p.V1 + 63) >> 6, sm, sref, sT,
                                  sB};
-            logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail, ss);
+            // (no peel for the sampled decode: +2.2 %, measured)
+            logit_stages<4, PAIRS, false>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail, ss);
         } else {
             logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail);
         }
@@ -2199,7 +2237,8 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         auto tail = [&]() __attribute__((always_inline)) {
             if (CROSS_PREFETCH && t < p.T) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
         };
-        logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, s0, s1, st, s64, pre && LOGIT_MIDSTORE, tail);
+        // (no peel here: +1.4 % at P = 64, the coop kernel's spills 28 -> 80)
+        logit_stages<4, PAIRS, false>(lds, p, nidx, c.wave, c.sgn, 0, hB, s0, s1, st, s64, pre && LOGIT_MIDSTORE, tail);
         cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && t < p.T;
         PROF_AT(blockIdx.x, 1024, pm + 1);
         // ---- phase A: this range's partial greedy state, write-through, then the group's merge
