@@ -571,7 +571,8 @@ def main():
                       'vector_share_of_iteration': round(mut_ms / (dt / args.steps * 1e3), 4),
                       'note': 'the per-task mutation vector, timed with events on the engine stream: SM-G-SUM '
                               '= nicnes_sum_sensitivity (the sigma 0 token decode + 95 batched backward passes of '
-                              'a 5-step decode, safe_mutations.py:93-117), SM-PROPORTIONAL = |theta| on the host'}
+                              'a 5-step decode, safe_mutations.py:93-117), SM-PROPORTIONAL = |theta| formed on the device '
+                              '(nicnes_set_mutation_proportional; the host mean only when theta has exact zeros)'}
                      if args.mutation else None),
         'update_ratio': ratio,
     }

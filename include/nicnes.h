@@ -120,6 +120,14 @@ int nicnes_noise_vectors(nicnes_handle* h, uint64_t iteration, int32_t member_be
 #define NICNES_MUTATION_DIVIDE 1
 #define NICNES_MUTATION_SCALE 2
 int nicnes_set_mutation(nicnes_handle* h, int32_t mode, const float* vec, void* stream);
+/* SM-PROPORTIONAL's vector from the handle's own fp32 theta (nets.py:108-112: |theta| with exact zeros replaced
+ * by mean|theta|), formed on the device: vec[j] = theta32[j] == 0 ? mean_abs : |theta32[j]|, then mode SCALE.
+ * mean_abs is the caller's fp32 mean of |theta| (the reference's torch mean, whose reduction order a device sum
+ * would not reproduce). Replaces a host round trip of theta through nicnes_set_mutation(SCALE, vec). */
+int nicnes_set_mutation_proportional(nicnes_handle* h, float mean_abs, void* stream);
+/* How many entries of the handle's fp32 theta are exactly zero (either sign): when none, SM-PROPORTIONAL's
+ * mean is not used and the caller can skip computing it. Synchronises the stream. */
+int nicnes_theta_zeros(nicnes_handle* h, int64_t* count_out_host, void* stream);
 
 /* Fitness criterion (Fitness enum + get_criterium, src/captioning/policies.py:22-61, applied at
  * :119-125): GREEDY = 100 * mean CIDEr-D; the greedy_* modes weight each step's probability of the

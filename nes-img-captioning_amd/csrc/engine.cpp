@@ -91,6 +91,7 @@ struct nicnes_handle {
     std::vector<double> su_host;      // nicnes_set_sample_draws (test hook): draws to use instead of the engine's
     int rpi = 1;                      // nicnes_set_rows_per_image: rows the sampled modes decode per image
     float* dscratch = nullptr;
+    unsigned long long* zcount = nullptr; // nicnes_theta_zeros: the count of exact zeros of theta32
     int32_t* stats = nullptr;
     int32_t* alive = nullptr;         // per decode workgroup: rows left unfinished (fused [stride], split [2][stride])
     int32_t alive_stride = 0;         // max decode workgroups (members x 64-row slabs)
@@ -434,7 +435,7 @@ int nicnes_destroy(nicnes_handle* h) {
                     h->ref_norm, h->nidx, h->seq, h->lp, h->row_scores, h->dscratch, h->stats, h->partials, h->norms,
                     h->hash_keys, h->hash_vals, h->img_hkey, h->img_hrow, h->img_vr, h->alive, h->part,
                     h->rank_key, h->rank_idx, h->mbatch, h->mut_vec, h->dbuf, h->didx, h->noise_sc, h->coop_ctr,
-                    h->zero_noise, h->zero_idx, h->sens_tok, h->su, h->base_scores, h->slog, h->slog_slots};
+                    h->zero_noise, h->zero_idx, h->sens_tok, h->su, h->base_scores, h->slog, h->slog_slots, h->zcount};
     if (h->sens) nicnes_sens_destroy(h->sens);
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -668,6 +669,40 @@ int nicnes_set_mutation(nicnes_handle* h, int32_t mode, const float* vec, void* 
     }
     if (mode) HIPC(h, hipMemcpyAsync(h->mut_vec, vec, (size_t)h->D * sizeof(float), hipMemcpyDeviceToDevice, s));
     h->mut_mode = mode;
+    return NICNES_OK;
+}
+
+int nicnes_set_mutation_proportional(nicnes_handle* h, float mean_abs, void* stream) {
+    if (!h || !(mean_abs >= 0.f)) return NICNES_ERR_INVALID;
+    if (!h->theta_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_theta first");
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    if (!h->mut_vec) {               // first use: the [D] vector
+        HIPC(h, hipDeviceSynchronize());
+        int rc = dalloc(h, &h->mut_vec, (size_t)h->D);
+        if (rc) return rc;
+    }
+    HIPC(h, nicnes_launch_proportional(h->theta32, h->D, mean_abs, h->mut_vec, s));
+    h->mut_mode = 2;
+    return NICNES_OK;
+}
+
+int nicnes_theta_zeros(nicnes_handle* h, int64_t* count_out_host, void* stream) {
+    if (!h || !count_out_host) return NICNES_ERR_INVALID;
+    if (!h->theta_set) return fail(h, NICNES_ERR_INVALID, "nicnes_set_theta first");
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(h, hipSetDevice(h->device));
+    if (!h->zcount) {
+        HIPC(h, hipDeviceSynchronize());
+        int rc = dalloc(h, &h->zcount, 1);
+        if (rc) return rc;
+    }
+    unsigned long long* d = h->zcount;
+    HIPC(h, nicnes_launch_count_zeros(h->theta32, h->D, d, s));
+    unsigned long long c = 0;
+    HIPC(h, hipMemcpyAsync(&c, d, sizeof c, hipMemcpyDeviceToHost, s));
+    HIPC(h, hipStreamSynchronize(s));
+    *count_out_host = (int64_t)c;
     return NICNES_OK;
 }
 

@@ -34,6 +34,9 @@ extern "C" hipError_t nicnes_launch_noise_vectors(const float* noise, const uint
                                                   float sigma, float* out, hipStream_t s);
 extern "C" hipError_t nicnes_launch_mutate(const float* noise, const uint64_t* idx, int count, int64_t dim, float sigma,
                                            const float* vec, int mode, float* out, int64_t out_stride, hipStream_t s);
+extern "C" hipError_t nicnes_launch_proportional(const float* theta, int64_t n, float mean_abs, float* out,
+                                                 hipStream_t s);
+extern "C" hipError_t nicnes_launch_count_zeros(const float* theta, int64_t n, unsigned long long* out, hipStream_t s);
 extern "C" hipError_t nicnes_launch_iota_stride(uint64_t* out, int n, uint64_t stride, hipStream_t s);
 extern "C" size_t nicnes_rank_scratch_pairs(int n);
 extern "C" hipError_t nicnes_launch_rank(const double* fit, int n, uint64_t* skey, uint32_t* sidx, double* cr_out,

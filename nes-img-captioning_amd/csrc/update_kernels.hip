@@ -435,6 +435,38 @@ extern "C" hipError_t nicnes_launch_mutate(const float* noise, const uint64_t* i
     return hipGetLastError();
 }
 
+// SM-PROPORTIONAL's vector (nets.py:108-112): |theta| with exact zeros (either sign) replaced by mean|theta|
+__global__ __launch_bounds__(256) void nicnes_proportional_kernel(const float* theta, int64_t n, float mean_abs,
+                                                                  float* out) {
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+        const float t = theta[j];
+        out[j] = t == 0.f ? mean_abs : __builtin_fabsf(t);
+    }
+}
+
+extern "C" hipError_t nicnes_launch_proportional(const float* theta, int64_t n, float mean_abs, float* out,
+                                                 hipStream_t s) {
+    hipLaunchKernelGGL(nicnes_proportional_kernel, dim3(2048), dim3(256), 0, s, theta, n, mean_abs, out);
+    return hipGetLastError();
+}
+
+// exact zeros of theta (an integer count: the order of the atomic adds does not change it)
+__global__ __launch_bounds__(256) void nicnes_count_zeros_kernel(const float* theta, int64_t n,
+                                                                 unsigned long long* out) {
+    unsigned long long c = 0;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+        c += theta[j] == 0.f ? 1ull : 0ull;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
+extern "C" hipError_t nicnes_launch_count_zeros(const float* theta, int64_t n, unsigned long long* out, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(nicnes_count_zeros_kernel, dim3(1024), dim3(256), 0, s, theta, n, out);
+    return hipGetLastError();
+}
+
 // the sigma-scaled table the decode kernels read: out[i] = fp32(sigma * table[i]), each member's
 // delta = fp32(sigma * z) (nets.py:102) then being a plain slice of it
 __global__ __launch_bounds__(256) void nicnes_scale_kernel(const float* in, float* out, uint64_t n, float sigma) {

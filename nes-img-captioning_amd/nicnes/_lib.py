@@ -20,6 +20,7 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_set_decode_split', 'nicnes_decode_shape', 'nicnes_set_decode_streams', 'nicnes_comm_unique_id', 'nicnes_comm_init',
            'nicnes_comm_attach', 'nicnes_comm_destroy', 'nicnes_comm_count', 'nicnes_clear_faults', 'nicnes_allgather_fitness', 'nicnes_allreduce_grad',
            'nicnes_noise_vectors', 'nicnes_set_batches', 'nicnes_evaluate_batches', 'nicnes_set_mutation',
+           'nicnes_set_mutation_proportional', 'nicnes_theta_zeros',
            'nicnes_set_decode_coop', 'nicnes_decode_path', 'nicnes_sum_sensitivity', 'nicnes_grad_partial_range',
            'nicnes_evaluate_theta', 'nicnes_set_sample_draws', 'nicnes_set_rows_per_image']
 
@@ -76,6 +77,8 @@ def lib(path=None):
         'nicnes_noise_vectors': (c.c_int, [vp, u64, i32, i32, f32, vp, vp]),
         'nicnes_set_batches': (c.c_int, [vp, vp, i32, i32, vp, i32, vp, vp]),
         'nicnes_set_mutation': (c.c_int, [vp, i32, vp, vp]),
+        'nicnes_set_mutation_proportional': (c.c_int, [vp, c.c_float, vp]),
+        'nicnes_theta_zeros': (c.c_int, [vp, vp, vp]),
         'nicnes_evaluate_batches': (c.c_int, [vp, u64, i32, i32, f32, vp, vp, vp, vp, vp]),
         'nicnes_evaluate_theta': (c.c_int, [vp, i32, u64, vp, vp, vp, vp]),
         'nicnes_set_sample_draws': (c.c_int, [vp, vp, i64]),

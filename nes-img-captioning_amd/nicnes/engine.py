@@ -197,6 +197,23 @@ class Engine:
         self._keep['mutation'] = v
         self.mutation_mode = code
 
+    def set_mutation_proportional(self, mean_abs):
+        """SM-PROPORTIONAL's vector formed on the device from the handle's fp32 theta
+        (nicnes_set_mutation_proportional): |theta| with exact zeros replaced by mean_abs, the caller's fp32
+        mean of |theta| (nets.py:108-112); then mode 'scale'."""
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_set_mutation_proportional(self.h, float(mean_abs), self._stream()), self.h,
+                  'set_mutation_proportional')
+        self._keep['mutation'] = None
+        self.mutation_mode = self.MUTATION_MODES['scale']
+
+    def theta_zeros(self):
+        """How many entries of the fp32 theta are exactly zero (nicnes_theta_zeros; synchronises)."""
+        out = ctypes.c_int64(0)
+        with torch.cuda.device(self.device):
+            check(self.L.nicnes_theta_zeros(self.h, ctypes.byref(out), self._stream()), self.h, 'theta_zeros')
+        return int(out.value)
+
     # Fitness enum values the engine implements (src/captioning/policies.py:22-35) -> nicnes.h codes
     FITNESS_MODES = {'greedy': 0, 'greedy_logprob': 1, 'greedy_expprob': 2, 'greedy_linprob': 3,
                      'greedy_avgprob': 4, 'sample': 5, 'self_critical': 6, 'sc_loss': 7}

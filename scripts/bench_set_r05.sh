@@ -5,10 +5,10 @@
 # configs[3] and configs[4] (their whole populations on one GPU), B = 64 (mscoco_nes.json's batch_size)
 # at P = 512 and 64, greedy_linprob, trained-like theta, 64 batches per iteration, SM-G-SUM / SM-PROPORTIONAL
 # and the sampled fitness modes.
-# usage (on the GPU box): bash scripts/bench_set_r04.sh TAG
+# usage (on the GPU box): bash scripts/bench_set_r05.sh TAG
 set -eo pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/${1:-benchset_r04}
+O=gpurun_out/${1:-benchset_r05}
 mkdir -p $O
 B="python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline"
 timeout -k 10 400 python3 -u bench.py > $O/bench_default.json 2> $O/bench_default.err
@@ -27,5 +27,6 @@ timeout -k 10 300 python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --m
 for F in sample self_critical sc_loss; do
   timeout -k 10 300 python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline --fitness $F > $O/bench_fitness_$F.json 2> $O/bench_fitness_$F.err
 done
+timeout -k 10 300 python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline --fitness sample --theta-gain 4 --bias-std 0.1 > $O/bench_sample_trained_like.json 2> $O/bench_sample_trained_like.err
 timeout -k 10 300 python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline --mutation SM-PROPORTIONAL > $O/bench_smprop.json 2> $O/bench_smprop.err
 echo done

@@ -222,3 +222,32 @@ def test_safe_mutation_master_trajectory_matches_oracle_engine():
         assert np.allclose(e.theta()[0].cpu().numpy(), ora_e.adam.theta, rtol=1e-6, atol=1e-12)
     finally:
         e.close()
+
+
+def test_proportional_vector_formed_on_the_device_equals_the_host_one():
+    """nicnes_set_mutation_proportional: |theta'| formed from the handle's own theta on the GPU (exact zeros of
+    either sign take the host's fp32 mean|theta|) gives the same delta' rows, bit for bit, as the host vector
+    of nets.py:108-112 passed through nicnes_set_mutation('scale'); the Mutator takes this path."""
+    import nicnes
+    from nicnes import mutations as MU
+    dims = O.Dims()
+    theta = O.make_theta(dims, 4, 4.0, 0.1)
+    theta[:dims.E * dims.F:7] = 0.0
+    theta[1:dims.E * dims.F:11] = -0.0
+    table = O.noise_table(NOISE_LEN, 123)
+    e = nicnes.Engine(max_batch=8, max_members=3, noise_len=NOISE_LEN, noise_seed=SEED)
+    try:
+        e.set_noise_table(table)
+        e.set_theta(theta)
+        e.set_mutation('scale', MU.proportional_vector(theta))
+        want = e.noise_vectors(IT, 0, 3, SIGMA).cpu().numpy()
+        e.set_mutation('plain')
+        e.set_mutation_proportional(float(MU.proportional_mean(e.theta()[1])))
+        got = e.noise_vectors(IT, 0, 3, SIGMA).cpu().numpy()
+        assert np.array_equal(got, want)
+        assert e.mutation_mode == 2
+        assert e.theta_zeros() == int((theta == 0).sum()) > 0
+        with pytest.raises(nicnes.NicnesError):
+            e.set_mutation_proportional(float('nan'))
+    finally:
+        e.close()
