@@ -96,13 +96,21 @@ def test_noise_sum_in_ranges_equals_whole(eng):
     assert torch.equal(out, g)
 
 
-@pytest.mark.parametrize('B,bu', [(130, False), (40, True)], ids=['two_slabs', 'bu_features'])
-def test_tokens_match_oracle(eng, B, bu):
+@pytest.mark.parametrize('B,bu,shape', [(130, False, (0, 0)), (40, True, (0, 0)), (128, True, (0, 0)),
+                                         (128, True, (1, 4)), (128, True, (4, 4))],
+                         ids=['two_slabs', 'bu_features', 'bu_b128_split', 'bu_b128_fused', 'bu_b128_S4'])
+def test_tokens_match_oracle(eng, B, bu, shape):
+    """Tokens of one member against the oracle; the 'bu' features (configs[4]) at B = 40 and at the bench's
+    B = 128 on the split path, the fused kernel's shape (S = 1) and the coop kernel's (S = 4, G = 4)."""
     dims = O.Dims()
     theta = O.make_theta(dims, 2, 4.0, 0.1)
     fc = _fc(B, 77, bu)
     _load(eng, theta, fc)
-    _, seq = eng.evaluate(6, 1, 1, SIGMA, return_seq=True)
+    eng.set_decode_split(*shape)
+    try:
+        _, seq = eng.evaluate(6, 1, 1, SIGMA, return_seq=True)
+    finally:
+        eng.set_decode_split(0, 0)
     seq = seq.cpu().numpy()[0]
     idx = int(eng.noise_indices(6, 1, 1).cpu().numpy()[0])
     rows = sorted({0, 31, 32, min(127, B - 1), B - 1} | ({128, 129} if B > 128 else set()))
