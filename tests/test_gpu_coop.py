@@ -204,3 +204,29 @@ def test_coop_repeated_launches_are_deterministic(monkeypatch, bounded):
         assert e.stats()['coop_timeouts'] == 0
     finally:
         e.close()
+
+
+def test_coop_needs_a_stage_per_range():
+    """a vocabulary of fewer 64-column logit stages than ranges (V1 = 128: two stages) never takes the coop
+    path, whose ranges must be non-empty; S = 2 still does, bit-identical to the split path"""
+    import nicnes
+    e = nicnes.Engine(vocab_size=127, max_batch=128, max_members=4, noise_len=NOISE_LEN, noise_seed=3)
+    try:
+        e.set_noise_table(O.noise_table(NOISE_LEN, 123))
+        rng = np.random.Generator(np.random.PCG64(9))
+        theta = (0.05 * rng.standard_normal(e.D)).astype(np.float32)
+        _load(e, theta, _fc(128, 77))
+        out = {}
+        for S, coop in ((4, 1), (2, 1), (2, 0)):
+            e.set_decode_split(S, 4)
+            e.set_decode_coop(coop)
+            out[S, coop] = (e.decode_path(128, 4), e.evaluate(1, 0, 4, SIGMA, return_seq=True, return_lp=True))
+        assert out[4, 1][0] == 'split' and out[2, 1][0] == 'coop' and out[2, 0][0] == 'split'
+        for a, b in zip(out[2, 1][1], out[2, 0][1]):
+            assert torch.equal(a, b)
+        assert torch.equal(out[4, 1][1][1], out[2, 0][1][1])     # tokens of the S = 4 split path (empty ranges)
+        assert e.stats()['coop_timeouts'] == 0
+    finally:
+        e.set_decode_coop(1)
+        e.set_decode_split(0, 0)
+        e.close()
