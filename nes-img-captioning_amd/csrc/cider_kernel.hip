@@ -95,15 +95,13 @@ struct NgramLane {
     double vec;     // tf * (ref_len - log(max(1, df)))   (counts2vec)
 };
 
-// per-lane n-gram of one caption row, its tf over the row, first-occurrence flag and weight
-__device__ __forceinline__ NgramLane ngram_lane(const int32_t* row, int T, int lane, const CiderTables& tb) {
-    NgramLane g;
-    const int L = caption_len(row, T);
+// per-lane n-gram of one caption row (L = caption_len), its tf over the row and first-occurrence flag
+__device__ __forceinline__ void ngram_key(const int32_t* row, int T, int lane, int L, NgramLane& g, int& tf) {
     int i;
     slot_of_lane(lane, g.n, i);
     g.valid = i + g.n <= L;
     g.key = g.valid ? pack_ngram(row, g.n, i) : 0ull;
-    int tf = 0;
+    tf = 0;
     bool first = g.valid;
     const int seg = lane & 48;
     for (int o = 0; o < 16; ++o) {             // equal keys have equal n: same segment
@@ -115,7 +113,14 @@ __device__ __forceinline__ NgramLane ngram_lane(const int32_t* row, int T, int l
     }
     g.first = first;
     g.vec = 0.0;
-    if (first) {
+}
+
+// ... and its weight
+__device__ __forceinline__ NgramLane ngram_lane(const int32_t* row, int T, int lane, const CiderTables& tb) {
+    NgramLane g;
+    int tf;
+    ngram_key(row, T, lane, caption_len(row, T), g, tf);
+    if (g.first) {
         const double df = df_lookup(tb, g.key);
         g.vec = (double)tf * (tb.ref_len - log(df > 1.0 ? df : 1.0));
     }
@@ -333,6 +338,9 @@ __global__ __launch_bounds__(64) void nicnes_img_ngram_kernel(const int32_t* img
 // Rows per workgroup: 32, or 8 when there are few candidates (64 members per GPU: 128 candidates), so that the
 // launch still has >= ~2048 workgroups to hide the probe latency (the P = 64 rollouts: DESIGN §5).
 #define CIDER_IMG_ROWS 32
+#ifndef CIDER_PAR_PROBE
+#define CIDER_PAR_PROBE 1          // the df and image-table probes of an n-gram issued together
+#endif
 #ifndef CIDER_WPE
 #define CIDER_WPE 0                // > 0: amdgpu_waves_per_eu bound of the image kernel (register budget)
 #endif
@@ -351,11 +359,47 @@ __global__ __launch_bounds__(256) CIDER_IMG_ATTR void nicnes_cider_img_kernel(co
     const double sigma2x2 = 2.0 * 6.0 * 6.0;
     for (int b = (int)blockIdx.y * rows_wg + wave; b < b_end; b += 4) {
         const int32_t* row = seq + ((size_t)cand * B + b) * T;
-        const NgramLane g = ngram_lane(row, T, lane, tb);
-        const double nh = sqrt(seg_sum(g.first ? g.vec * g.vec : 0.0));
         const int L = caption_len(row, T);
         const int len_h = L > 1 ? L - 1 : 0;
         const int im = img0 + b / rpi;                                     // row b's image
+#if CIDER_PAR_PROBE
+        // the df probe and the image-table probe of the lane's n-gram both need only its key: their loads are
+        // issued together (one dependent round trip less per row than df first, then the image table)
+        const int rs0 = img_ref_start[im], rs1 = img_ref_start[im + 1];
+        int rl2[IMG_MAXR];
+        double rnm[IMG_MAXR];
+#pragma unroll
+        for (int u = 0; u < IMG_MAXR; ++u) {
+            rl2[u] = rs0 + u < rs1 ? tb.ref_len2[rs0 + u] : 0;
+            rnm[u] = rs0 + u < rs1 ? tb.ref_norm[(size_t)(rs0 + u) * 4 + (lane >> 4)] : 0.0;
+        }
+        NgramLane g;
+        int tf;
+        ngram_key(row, T, lane, L, g, tf);
+        int trow = -1;
+        double df = 0.0;
+        if (g.first) {
+            const uint64_t hs = df_hash(g.key);
+            uint64_t h = hs & tb.hash_mask;
+            uint32_t slot = (uint32_t)hs & (IMG_CAP - 1);
+            const uint64_t* ik = tb.img_hkey + (size_t)im * IMG_CAP;
+            uint64_t k1 = tb.hash_keys[h], k2 = ik[slot];
+            for (uint64_t probe = 0; probe < tb.hash_mask && k1 != g.key && k1 != 0ull; ++probe) {
+                h = (h + 1) & tb.hash_mask;
+                k1 = tb.hash_keys[h];
+            }
+            for (int probe = 0; probe < IMG_CAP - 1 && k2 != g.key && k2 != 0ull; ++probe) {
+                slot = (slot + 1) & (IMG_CAP - 1);
+                k2 = ik[slot];
+            }
+            if (k1 == g.key) df = tb.hash_vals[h];
+            if (k2 == g.key) trow = tb.img_hrow[(size_t)im * IMG_CAP + slot];
+            g.vec = (double)tf * (tb.ref_len - log(df > 1.0 ? df : 1.0));
+        }
+        const double nh = sqrt(seg_sum(g.first ? g.vec * g.vec : 0.0));
+#else
+        const NgramLane g = ngram_lane(row, T, lane, tb);
+        const double nh = sqrt(seg_sum(g.first ? g.vec * g.vec : 0.0));
         int trow = -1;
         if (g.first) {
             uint32_t slot = (uint32_t)df_hash(g.key) & (IMG_CAP - 1);
@@ -366,8 +410,26 @@ __global__ __launch_bounds__(256) CIDER_IMG_ATTR void nicnes_cider_img_kernel(co
                 slot = (slot + 1) & (IMG_CAP - 1);
             }
         }
+#endif
         const double* vrow = tb.img_vr + ((size_t)im * IMG_ROWS + (trow >= 0 ? trow : 0)) * IMG_MAXR;
         double score = 0.0;
+#if CIDER_PAR_PROBE
+        // (r1 - r0 <= IMG_MAXR on this path: the engine takes it only then) the image's reference terms, loaded
+        // before the probes' results are waited for
+        const int r0 = rs0, r1 = rs1;
+#pragma unroll
+        for (int u = 0; u < IMG_MAXR; ++u) {
+            if (r0 + u >= r1) break;
+            const double vr = trow >= 0 ? vrow[u] : 0.0;
+            const double contrib = g.first ? (g.vec < vr ? g.vec : vr) * vr : 0.0;
+            const double delta = (double)(len_h - rl2[u]);
+            const double pen = exp(-(delta * delta) / sigma2x2);
+            double val = seg_sum(contrib);
+            const double nr = rnm[u];
+            if (nh != 0.0 && nr != 0.0) val /= (nh * nr);
+            score += val * pen;
+        }
+#else
         const int r0 = img_ref_start[im], r1 = img_ref_start[im + 1];
         for (int r = r0; r < r1; ++r) {
             const double vr = trow >= 0 ? vrow[r - r0] : 0.0;
@@ -379,6 +441,7 @@ __global__ __launch_bounds__(256) CIDER_IMG_ATTR void nicnes_cider_img_kernel(co
             if (nh != 0.0 && nr != 0.0) val /= (nh * nr);
             score += val * pen;
         }
+#endif
         score += __shfl_xor(score, 16);
         score += __shfl_xor(score, 32);
         if (lane == 0) {
