@@ -207,10 +207,10 @@ def test_coop_repeated_launches_are_deterministic(monkeypatch, bounded):
 
 
 def test_coop_needs_a_stage_per_range():
-    """a vocabulary of fewer 64-column logit stages than ranges (V1 = 128: two stages) never takes the coop
-    path, whose ranges must be non-empty; S = 2 still does, bit-identical to the split path"""
+    """the coop path needs a non-empty logit range per workgroup: V1 = 192 (three 64-column stages) takes it at
+    S = 2 but not at S = 4, bit-identical to the split path"""
     import nicnes
-    e = nicnes.Engine(vocab_size=127, max_batch=128, max_members=4, noise_len=NOISE_LEN, noise_seed=3)
+    e = nicnes.Engine(vocab_size=191, max_batch=128, max_members=4, noise_len=NOISE_LEN, noise_seed=3)
     try:
         e.set_noise_table(O.noise_table(NOISE_LEN, 123))
         rng = np.random.Generator(np.random.PCG64(9))
