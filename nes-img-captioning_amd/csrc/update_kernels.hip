@@ -399,6 +399,9 @@ __device__ __forceinline__ float mutate1(float z, float sigma, float v, int mode
 
 // VEC: 4 consecutive parameters per thread and one 16-byte store (the member's table slice starts at any float:
 // its loads stay dword-aligned 16-byte loads); the same per-element arithmetic as the scalar form
+#ifndef MUTATE_NT
+#define MUTATE_NT 0         // 1: the delta' rows written with nontemporal stores (A/B: scripts/gpu_r05_libstats.sh)
+#endif
 template <bool VEC>
 __global__ __launch_bounds__(256) void nicnes_mutate_kernel(const float* noise, const uint64_t* idx, int64_t dim,
                                                             float sigma, const float* vec, int mode, float* out,
@@ -416,7 +419,11 @@ __global__ __launch_bounds__(256) void nicnes_mutate_kernel(const float* noise, 
             const f32x4 vv = reinterpret_cast<const f32x4*>(vec)[i];
 #pragma unroll
             for (int e = 0; e < 4; ++e) r[e] = mutate1(zv[e], sigma, vv[e], mode);
+#if MUTATE_NT
+            __builtin_nontemporal_store(r, reinterpret_cast<f32x4*>(o) + i);   // (the decode re-reads it from HBM)
+#else
             reinterpret_cast<f32x4*>(o)[i] = r;
+#endif
         }
         j0 = 4 * n4;
     }
