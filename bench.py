@@ -215,14 +215,61 @@ def free_port():
         return s.getsockname()[1]
 
 
+VISIBLE_DEVICE_VARS = ('ROCR_VISIBLE_DEVICES', 'HIP_VISIBLE_DEVICES', 'CUDA_VISIBLE_DEVICES')
+
+
+def usable_gpu_count(env, topology='/sys/class/kfd/kfd/topology/nodes', dri='/dev/dri'):
+    """GPUs the rank processes could use, counted WITHOUT any HIP / HSA call (the launcher must not
+    initialise the GPU runtime: it only starts fresh rank processes). A GPU is a KFD topology node with
+    SIMDs whose DRM render node this process can open (a cgroup that hides a GPU makes the open fail);
+    a *_VISIBLE_DEVICES list caps the count. None when the topology cannot be read."""
+    try:
+        names = os.listdir(topology)
+    except OSError:
+        return None
+    n = 0
+    for name in sorted(names):
+        props = {}
+        try:
+            with open(os.path.join(topology, name, 'properties')) as f:
+                for line in f:
+                    parts = line.split()
+                    if len(parts) == 2:
+                        props[parts[0]] = parts[1]
+        except OSError:
+            continue
+        if int(props.get('simd_count', '0')) <= 0:
+            continue                               # a CPU node
+        minor = props.get('drm_render_minor')
+        if minor is None:
+            continue
+        try:
+            fd = os.open(os.path.join(dri, 'renderD%s' % minor), os.O_RDWR | os.O_CLOEXEC)
+            os.close(fd)
+        except OSError:
+            continue
+        n += 1
+    for var in VISIBLE_DEVICE_VARS:
+        val = env.get(var)
+        if val is not None:
+            n = min(n, len([v for v in val.split(',') if v.strip()]))
+    return n
+
+
 def launch_ranks(n, argv, grace=30.0):
     """Start n fresh rank processes running this script with `argv` (this process never touches the
-    GPU), wait for all of them, and return the exit status: 0, or the first failing rank's (a rank
-    killed by a signal counts as 1). When one rank fails the others are terminated."""
+    GPU: devices are counted from sysfs, usable_gpu_count), wait for all of them, and return the exit
+    status: 0, or the first failing rank's (a rank killed by a signal counts as 1). When one rank fails
+    the others are terminated. Status 2, before any rank starts, when fewer than n GPUs are usable or
+    they cannot be counted."""
     shared = os.environ.get('NICNES_BENCH_SHARE_GPU') == '1'
     if not shared:
-        import torch
-        have = torch.cuda.device_count()          # counts devices without initialising HIP
+        have = usable_gpu_count(os.environ, os.environ.get('NICNES_BENCH_KFD_TOPOLOGY',
+                                                           '/sys/class/kfd/kfd/topology/nodes'),
+                                os.environ.get('NICNES_BENCH_DRI', '/dev/dri'))
+        if have is None:
+            print('bench.py: --gpus %d: cannot read the KFD topology to count GPUs' % n, file=sys.stderr, flush=True)
+            return 2
         if have < n:
             print('bench.py: --gpus %d but %d GPUs are visible' % (n, have), file=sys.stderr, flush=True)
             return 2
@@ -301,14 +348,6 @@ def main():
     world, launch_here = resolve_world(args.gpus, os.environ)
     if launch_here:
         raise SystemExit(launch_ranks(world, sys.argv[1:]))
-    if os.environ.get('NICNES_BENCH_DRY_RANKS') == '1':
-        # test hook (tests/test_bench_launcher.py): report the rank environment and stop before any GPU work
-        print(json.dumps({k: os.environ.get(k) for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR',
-                                                          'MASTER_PORT')}), flush=True)
-        fail = os.environ.get('NICNES_BENCH_DRY_FAIL_RANK')
-        if fail is not None and fail == os.environ.get('RANK'):
-            raise SystemExit(3)
-        return
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     P_pre, B_pre, bu_pre, cfg_text = PRESETS[args.preset]
@@ -322,6 +361,17 @@ def main():
         if P % world:
             raise SystemExit('population %d does not split evenly over %d GPUs' % (P, world))
         P_local = P // world
+    if os.environ.get('NICNES_BENCH_DRY_RANKS') == '1':
+        # test hook (tests/test_bench_launcher.py): report the rank environment and the member range this rank
+        # would evaluate (PopulationRunner's m0 = rank x P / N), then stop before any GPU work
+        rec = {k: os.environ.get(k) for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')}
+        rec.update(members=[rank * P_local, (rank + 1) * P_local], population=P, batch=B, bu=bool(args.bu),
+                   scaling=scaling)
+        print(json.dumps(rec), flush=True)
+        fail = os.environ.get('NICNES_BENCH_DRY_FAIL_RANK')
+        if fail is not None and fail == os.environ.get('RANK'):
+            raise SystemExit(3)
+        return
 
     # CPU leg first, before this process touches the GPU (its pool forks)
     cpu = None

@@ -857,6 +857,7 @@ __global__ __launch_bounds__(1024) void sens_emb_part(const float* dX, const int
     const int j0 = runs[1 + lo] + EMB_CH * (c - rchunk[lo]), j1 = min(j0 + EMB_CH, runs[2 + lo]);
     const int64_t sk = (int64_t)(L + 1) * Bs * E;
     const int k0 = kl * EMB_KPR2;
+    if (k0 >= K) return;                                         // small vocabularies: this k lane has no seeds
     float acc[EMB_KPR2];
 #pragma unroll
     for (int q = 0; q < EMB_KPR2; ++q) acc[q] = 0.f;
@@ -1225,7 +1226,8 @@ extern "C" int nicnes_sens_run(SensWork* w, const SensParams* p, hipStream_t st)
                            Cs(i), i ? (const float*)Cs(i - 1) : (const float*)nullptr, dSi, sdk, K, Bs, R);
         // dX_i = dS_i Wi ([5R, E] row-major), dH_{i-1} = dS_i Wh: one launch of both (Wi, Wh stay put over k), 2 seeds
         // per workgroup (4 x (1 or 2) x 32 workgroups at Bs = 128, K = 95); the tile kernel with NICNES_SENS_TILE_BWD
-        if (E == R && E <= 128 && !env_on("NICNES_SENS_TILE_BWD") && bsq_fits(sa(dSi, sdk, G5, 1), Bs, G5, Wi, E, E) &&
+        // (the fused launch puts dH's columns at the second 128-column tile: E == R == 128 exactly)
+        if (E == R && E == 128 && !env_on("NICNES_SENS_TILE_BWD") && bsq_fits(sa(dSi, sdk, G5, 1), Bs, G5, Wi, E, E) &&
             al(Wh)) {
             const int kb2 = 2, nzb = (K + kb2 - 1) / kb2;
             hipLaunchKernelGGL((sens_bsq<false, 2>), dim3(blocks(Bs, 32), i >= 1 ? 2 : 1, nzb), dim3(256), 0, st,

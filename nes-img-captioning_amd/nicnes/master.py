@@ -210,6 +210,7 @@ class EngineMaster:
             for batch in self._batch_stream(batches):
                 yielded = True
                 t0 = time.time()
+                before = dict(self.sched.__dict__)      # the schedule a fault snapshot must record
                 self.sched.incr_iteration()
                 self._set_batch(batch)
                 self._prepare_mutation(batch)
@@ -223,6 +224,10 @@ class EngineMaster:
                     except DecodeFault as err:
                         self._record_fault(err, attempt, self.e.clear_faults())
                         if attempt == int(fault_retries):
+                            # theta / m / v are those before the faulted iteration, so the snapshot records the
+                            # schedule as it was then too (a curriculum step taken by incr_iteration undone):
+                            # resuming from it replays the faulted iteration exactly once
+                            self.sched.__dict__.update(before)
                             if self.rank == 0:
                                 self.save_snapshot()
                             raise

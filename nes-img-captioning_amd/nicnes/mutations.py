@@ -105,17 +105,18 @@ class Mutator:
         if not self.active or key == self._key:
             return self.vector
         if self.mode == 'SM-PROPORTIONAL':
-            if callable(theta32):
-                theta32 = theta32()
+            def theta_now():
+                return theta32() if callable(theta32) else theta32
             if hasattr(self.e, 'set_mutation_proportional'):
                 # the engine forms |theta'| from its own theta on the device; the host computes only the mean,
                 # and only when theta has exact zeros for it to replace (4.1 ms a task with the vector's host
-                # round trip at D = 2.87 M; 1.9 ms with the mean; tens of us without)
-                mean = float(proportional_mean(theta32)) if self.e.theta_zeros() else 0.0
+                # round trip at D = 2.87 M; 1.9 ms with the mean; tens of us without). theta is read only then.
+                mean = float(proportional_mean(theta_now())) if self.e.theta_zeros() else 0.0
                 self.e.set_mutation_proportional(mean)
                 self.vector = None
             else:
-                th = theta32.detach().cpu().numpy() if isinstance(theta32, torch.Tensor) else np.asarray(theta32)
+                th = theta_now()
+                th = th.detach().cpu().numpy() if isinstance(th, torch.Tensor) else np.asarray(th)
                 self.vector = proportional_vector(th.astype(np.float32, copy=False))
                 self.e.set_mutation('scale', self.vector)
         else:

@@ -27,7 +27,10 @@ Fixtures (all .npz, loadable with allow_pickle=False):
                                   whether the 5 copies of every image decoded identically
   decode_bench_b64.npz            the same at mscoco_nes.json's own batch_size 64 (experiments/mscoco_nes.json:7):
                                   the first 64 images (320 duplicated rows), the 64-row slab path of the engine
-  master_ranks_grad.npz           NESMaster.compute_centered_ranks / gradient_estimate
+  decode_rank_slices.npz          the per-GPU slices of the 8-GPU configs: configs[3] rank 7 (members 1792-2047
+                                  of pop 2048) on the bench inputs, configs[4] rank 7 (members 448-511, plus
+                                  members of rank 0) on bottom-up ReLU(N(0,1)) features (fc seed 1235)
+  master_ranks_grad.npz          NESMaster.compute_centered_ranks / gradient_estimate
                                   (nic_nes_master.py:170-221) imported with placeholder redis/torchvision
                                   modules: P = 512 tie-free fitness and a tied one, and the fp32 gradient
                                   of 512 table-noise vectors on 4096 sampled coordinates
@@ -251,6 +254,50 @@ def decode_sample_fixture():
 
 def decode_bench_b64_fixture():
     decode_bench_fixture(64, 'decode_bench_b64')
+
+
+# the last rank's slice of each multi-GPU BASELINE config (member ranges as bench.py --gpus 8 shards them)
+SLICE_C3 = np.array([1792, 1793, 1830, 1871, 1920, 1966, 2001, 2047], np.int64)       # configs[3]: P=2048, rank 7
+SLICE_C4 = np.array([0, 7, 33, 63, 448, 449, 470, 490, 511], np.int64)               # configs[4]: P=512, rank 7 (+ rank 0)
+
+
+def decode_rank_slices_fixture():
+    """decode_rank_slices.npz: FCModel._sample on the per-GPU slices of the two 8-GPU BASELINE configs.
+    c3 = configs[3] (pop = 2048 over 8 GPUs: rank 7 evaluates members 1792..2047) on the bench inputs (xavier
+    theta seed 0, fc PCG64(1234) N(0,1), B = 128, 5x-duplicated rows); c4 = configs[4] (bottom-up features:
+    ReLU of PCG64(1235) N(0,1), nicnes.synthetic.fc_feats(bu=True); pop = 512 over 8 GPUs: rank 7 evaluates
+    members 448..511, plus members of rank 0's slice). Same table / noise seed / iteration / sigma as
+    decode_bench_xavier. Per case: seq [1 + 2 * members, B, T] (base theta first, then m+, m- per member) of
+    each image's first copy, margins, logprobs, dup_consistent."""
+    d = O.Dims()
+    model = ref_model(d)
+    theta = O.make_theta(d, 0, 1.0, 0.0)
+    T_LEN, TSEED, NSEED, IT, SIGMA, B = 1 << 27, 123, 0, 1, 0.01, 128
+    table = O.noise_table(T_LEN, TSEED)
+    out = dict(B=np.int64(B), noise_len=np.int64(T_LEN), table_seed=np.int64(TSEED), noise_seed=np.int64(NSEED),
+               iteration=np.int64(IT), sigma=np.float64(SIGMA))
+    for case, fc_seed, bu, members in (('c3', 1234, False, SLICE_C3), ('c4', 1235, True, SLICE_C4)):
+        fc = np.random.Generator(np.random.PCG64(fc_seed)).standard_normal((B, d.F)).astype(np.float32)
+        if bu:
+            fc = np.maximum(fc, 0.0).astype(np.float32)
+        fc5 = np.repeat(fc, 5, axis=0)
+        seqs, mars, lps, dup = [], [], [], []
+        for k in range(-1, len(members)):
+            for sign in ((0,) if k < 0 else (+1, -1)):
+                th = theta if k < 0 else O.perturb(theta, table, O.noise_index(NSEED, IT, int(members[k]), T_LEN,
+                                                                                d.D), SIGMA, sign)
+                load_theta(model, th)
+                s5, lp5, m5 = ref_decode(model, fc5)
+                s5, lp5, m5 = s5.reshape(B, 5, -1), lp5.reshape(B, 5, -1), m5.reshape(B, 5, -1)
+                dup.append(bool((s5 == s5[:, :1]).all()))
+                seqs.append(s5[:, 0])
+                mars.append(m5[:, 0])
+                lps.append(lp5[:, 0])
+        out.update({case + '_fc_seed': np.int64(fc_seed), case + '_bu': np.bool_(bu), case + '_members': members,
+                    case + '_seq': np.stack(seqs).astype(np.int16), case + '_margins': np.stack(mars),
+                    case + '_logprobs': np.stack(lps), case + '_dup_consistent': np.array(dup)})
+        print('rank slice', case, 'copies consistent', all(dup), 'min margin', float(np.stack(mars).min()))
+    np.savez_compressed(os.path.join(OUT, 'decode_rank_slices.npz'), **out)
 
 
 class _Placeholder(__import__('types').ModuleType):
@@ -487,6 +534,7 @@ def all_fixtures():
     fitness_criteria_fixture()
     decode_bench_fixture()
     decode_bench_b64_fixture()
+    decode_rank_slices_fixture()
     master_ranks_grad_fixture()
     wire_fixture()
     mutations_fixture()

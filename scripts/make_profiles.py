@@ -1,4 +1,4 @@
-"""Turn one profile_r03.sh run (gpurun_out/<TAG>/) into the committed profile files (dev tool):
+"""Turn one profile.sh run (gpurun_out/<TAG>/) into the committed profile files (dev tool):
   profiles/<round>_kernel_stats_p<P>.csv       rocprofv3 --kernel-trace --stats summary of the bench
   profiles/<round>_decode_launches_p<P>.json   full-population launch averages (scripts/trace_summary.py)
   profiles/<round>_pmc_<key>_p<P>_b128.json    per-launch PMC counters + derived figures (pmc_summary.py),

@@ -3,7 +3,7 @@
 # (the strong-scaling shapes: P = 512 fused steps kernel, P = 128 / 64 coop kernel), then per P four PMC
 # passes (each within the per-pass slot limits of MI355X_MICROARCH.md: <= 8 SQ, <= 2 GRBM, FETCH_SIZE /
 # WRITE_SIZE alone). Raw CSVs go to gpurun_out/<TAG>/; scripts/make_profiles.py post-processes them.
-# usage (on the GPU box): bash scripts/profile_r03.sh TAG "512 128 64" [extra bench args]
+# usage (on the GPU box): bash scripts/profile.sh TAG "512 128 64" [extra bench args]
 set -eo pipefail
 TAG=${1:-r03}
 PS=${2:-"512 128 64"}

@@ -551,7 +551,44 @@ def test_master_reruns_a_contained_fault(workload, tmp_path):
     with pytest.raises(nicnes.DecodeFault):
         m2.run([(fc, gts)] * 3, max_iterations=3, fault_retries=1)
     assert [(f['iter'], f['attempt']) for f in m2.faults] == [(1, 0), (1, 1)] and m2.stats == []
-    assert list((tmp_path / 'f2' / 'snapshot').glob('z_info_e1_i1-0.json'))
+    # the snapshot records the state before the faulted iteration 1 (iteration 0), theta / m / v included
+    assert list((tmp_path / 'f2' / 'snapshot').glob('z_info_e1_i0-0.json'))
+
+
+def test_fault_snapshot_at_a_schedule_boundary_records_the_pre_fault_schedule(workload, tmp_path):
+    """when the faulted iteration is a curriculum boundary, incr_iteration has already divided sigma and
+    grown the batch; the fault snapshot must hold the schedule as it was before (matching theta, m, v), i.e. equal
+    the snapshot an unfaulted run writes after the previous iteration, so resuming does not step the curriculum
+    twice."""
+    import json as _json
+    import nicnes
+    dims, theta, fc, gts, df, n, table = workload
+    P = 4
+    cfg = dict(schedule_start=1, schedule_limit=2, stdev_divisor=2, bs_multiplier=2)   # boundaries at it = 1, 3
+    ref = M.EngineMaster(_sched_spec(P, 4, **cfg), OracleEngine(dims, theta, fc, gts, df, n, table),
+                         log_dir=str(tmp_path / 'ref'))
+    ref.run([(fc, gts)] * 2, max_iterations=2)
+    want = _json.loads(open(ref.save_snapshot()).read())
+    e = _FaultingEngine(dims, theta, fc, gts, df, n, table, faults=0)
+    m = M.EngineMaster(_sched_spec(P, 4, **cfg), e, log_dir=str(tmp_path / 'f'))
+    m.run([(fc, gts)] * 2, max_iterations=2)
+    e.faults_left = 2                                   # iteration 3 (a boundary) faults on both tries
+    with pytest.raises(nicnes.DecodeFault):
+        m.run([(fc, gts)] * 2, max_iterations=3, fault_retries=1)
+    [snap] = list((tmp_path / 'f' / 'snapshot').glob('z_info_*.json'))
+    got = _json.loads(snap.read_text())
+    for k in ('iter', 'noise_stdev', 'batch_size', 'times_orig_bs', 'nb_samples_used', 'bad_generations'):
+        assert got[k] == want[k], k
+    assert got['noise_stdev'] == 0.05 / 2 and got['iter'] == 2
+    # resuming replays the schedule exactly as the unfaulted run's snapshot would
+    r = M.Schedule(_sched_spec(P, 4, **cfg).config, P)
+    r.init_from_infos(got)
+    r.incr_iteration()
+    ref.sched.init_from_infos(want)
+    ref.sched.incr_iteration()
+    a, b = r.to_dict(), ref.sched.to_dict()
+    a.pop('epoch'), b.pop('epoch')                       # the faulted master ran two passes (two run() calls)
+    assert a == b
 
 
 def test_eval_rollout_draw_streams_differ_between_processes(workload):

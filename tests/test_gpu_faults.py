@@ -241,7 +241,7 @@ def test_master_gives_up_after_the_retries_with_a_snapshot(monkeypatch, tmp_path
         _master_run(monkeypatch, tmp_path, 2, iterations=1, retries=1)
     assert sorted(os.path.basename(p) for p in glob.glob(str(tmp_path / 'faults' / '*.json'))) == \
         ['fault_i1_a0.json', 'fault_i1_a1.json']
-    assert glob.glob(str(tmp_path / 'snapshot' / 'z_info_e*_i1-0.json'))
+    assert glob.glob(str(tmp_path / 'snapshot' / 'z_info_e*_i0-0.json'))    # the pre-fault state: iteration 0
     assert os.path.exists(tmp_path / 'snapshot' / 'optimizer.tar')
     from nicnes import nes as N
     st = N._load_state(str(tmp_path / 'snapshot' / 'optimizer.tar'))

@@ -125,6 +125,34 @@ def test_gpu_sensitivity_matches_oracle(theta_kind, rows):
     print('max relative error over entries >= 1e-3 max: %.3g' % worst)
 
 
+@pytest.mark.parametrize('vocab,theta_kind', [(999, 'wc'), (511, 'wc'), (511, 'xavier'), (127, 'xavier')])
+def test_gpu_sensitivity_small_vocabulary(vocab, theta_kind):
+    """a vocabulary below ~8,400 words has fewer seeds than the embedding kernels' 8 k lanes x 12 cover
+    (K = V1 / 100 + 1 = 11 at 999 words, 6 at 511, 2 at 127): the lanes past K must not read beyond dX. The vector
+    matches the restatement oracle within the full-vocabulary bar. (Below ~500 words with the peaked theta, and at
+    63 words with either, single-seed square sums amplify fp32 summation-order rounding to 1-2x the bar in a few
+    i2h entries: scripts/debug_sens_vocab.py; the reference vocabulary is 9,487 words.)"""
+    import nicnes
+    from oracle import sensitivity_ref as SR
+    dims = O.Dims(vocab_size=vocab)
+    theta = O.make_theta(dims, 3, 4.0, 0.1) if theta_kind == 'wc' else O.make_theta(dims, 0, 1.0, 0.0)
+    rows = 12
+    fc = np.random.Generator(np.random.PCG64(78)).standard_normal((rows, dims.F)).astype(np.float32)
+    e = nicnes.Engine(vocab_size=vocab, max_batch=rows, max_members=2, noise_len=NOISE_LEN, noise_seed=0)
+    try:
+        e.set_noise_table(O.noise_table(NOISE_LEN, 123))
+        e.set_theta(theta)
+        e.set_df_table(np.zeros(0, np.uint64), np.zeros(0), np.log(64.0))
+        e.set_batch(fc, [np.zeros((1, dims.T), np.int32)] * rows)
+        raw = e.sum_sensitivity(rows).cpu().numpy()
+        assert np.array_equal(e.sum_sensitivity(rows).cpu().numpy(), raw)
+    finally:
+        e.close()
+    ref = SR.sum_sensitivity((dims.vocab_size + 1, dims.E, dims.R, dims.F), theta, fc, rows).numpy()
+    ok, worst = _sens_close(raw, ref)
+    assert ok, worst
+
+
 @pytest.mark.parametrize('twin', ['before', 'after'])
 def test_sensitivity_greedy_tokens_at_planted_ties(twin):
     """the SM-G-SUM forward picks its own greedy tokens (sens_greedy). For every distinct first token a

@@ -108,6 +108,53 @@ def test_tokens_and_fitness_match_reference(goldens, P, name):
         e.close()
 
 
+@pytest.mark.parametrize('case, begin, count, path', [('c3', 1792, 256, 'fused'), ('c4', 448, 64, 'coop'),
+                                                      ('c4', 0, 64, 'coop')],
+                         ids=['configs3_rank7_of8', 'configs4_bu_rank7_of8', 'configs4_bu_rank0_of8'])
+def test_rank_slices_match_reference(golden_dir, case, begin, count, path):
+    """The exact per-GPU slice an 8-GPU run of configs[3] / configs[4] evaluates on one rank
+    (evaluate(it, begin, count) with bench.py's member ranges), against FCModel._sample of the imported
+    reference on the same members (tests/golden/decode_rank_slices.npz). configs[4] uses bottom-up ReLU
+    features and runs on the coop path (64 members per GPU at B = 128, S = 4); configs[3] on the fused path."""
+    import nicnes
+    import nicnes.synthetic as S
+    z = np.load(golden_dir + '/decode_rank_slices.npz')
+    members = z[case + '_members']
+    ref, mar = z[case + '_seq'].astype(np.int32), z[case + '_margins']
+    e = nicnes.Engine(max_batch=128, max_members=count, noise_len=int(z['noise_len']),
+                      noise_seed=int(z['noise_seed']))
+    try:
+        wl = S.setup_engine_workload(e, B=int(z['B']), fc_seed=int(z[case + '_fc_seed']), bu=bool(z[case + '_bu']),
+                                     noise=S.noise_table(int(z['noise_len']), int(z['table_seed'])))
+        full, upto = _agree(wl['base'], ref[0], mar[0])
+        assert full == ref.shape[1], 'base-theta decode differs from the reference'
+        assert e.decode_path(int(z['B']), count) == path
+        fit, seq = e.evaluate(int(z['iteration']), begin, count, float(z['sigma']), return_seq=True)
+        fit, seq = fit.cpu().numpy(), seq.cpu().numpy()
+        scorer = CR.CiderDOracle(wl['df'], wl['ref_len_raw'])
+        rows = rows_full = 0
+        fdiff = 0.0
+        for k, mbr in enumerate(members):
+            if not begin <= mbr < begin + count:
+                continue
+            for s in range(2):
+                r, m = ref[1 + 2 * k + s], mar[1 + 2 * k + s]
+                full, upto = _agree(seq[mbr - begin, s], r, m)
+                assert full == r.shape[0], (case, int(mbr), s, full)
+                rows += r.shape[0]
+                rows_full += full
+                fdiff = max(fdiff, abs(fit[mbr - begin, s] - CR.rollout_fitness(scorer, r, wl['gts'])[0]))
+        assert rows >= 4 * 2 * 128
+        assert fdiff <= 1e-9 * max(1.0, float(np.abs(fit).max()))
+        _report['%s_members_%d_%d' % (case, begin, begin + count)] = {
+            'decode_path': path, 'decode_shape': list(e.decode_shape(int(z['B']), count)), 'rows_compared': rows,
+            'rows_identical_end_to_end': rows_full, 'near_tie_steps_in_golden': int((mar[1:] < MARGIN).sum()),
+            'max_abs_fitness_diff_vs_reference_tokens': fdiff}
+        _write_report()
+    finally:
+        e.close()
+
+
 def test_ranks_and_gradient_match_reference(golden_dir):
     import nicnes
     z = np.load(golden_dir + '/master_ranks_grad.npz')

@@ -179,6 +179,29 @@ def test_bench_workload_decode_matches_reference(golden_dir, name):
         assert np.allclose(lp[live], z['logprobs'][k][live], atol=5e-6)
 
 
+@pytest.mark.parametrize('case', ['c3', 'c4'])
+def test_rank_slice_decode_matches_reference(golden_dir, case):
+    """decode_rank_slices.npz: the oracle on the per-GPU slices of the 8-GPU configs (configs[3] rank 7,
+    configs[4] rank 7 + rank 0 on bottom-up ReLU features) against FCModel._sample, every row end to end."""
+    z = np.load(golden_dir + '/decode_rank_slices.npz')
+    assert z[case + '_dup_consistent'].all()
+    d = O.Dims()
+    theta = O.make_theta(d, 0, 1.0, 0.0)
+    fc = np.random.Generator(np.random.PCG64(int(z[case + '_fc_seed']))).standard_normal(
+        (int(z['B']), d.F)).astype(np.float32)
+    if bool(z[case + '_bu']):
+        fc = np.maximum(fc, 0.0).astype(np.float32)
+    table = O.noise_table(int(z['noise_len']), int(z['table_seed']))
+    thetas = [theta]
+    for mbr in z[case + '_members']:
+        idx = O.noise_index(int(z['noise_seed']), int(z['iteration']), int(mbr), int(z['noise_len']), d.D)
+        thetas += [O.perturb(theta, table, idx, float(z['sigma']), sign) for sign in (+1, -1)]
+    ref = z[case + '_seq'].astype(np.int32)
+    for k, th in enumerate(thetas):
+        seq, _, _ = O.decode(d, th, fc)
+        assert np.array_equal(seq, ref[k]), (case, k, np.argwhere(seq != ref[k])[:3])
+
+
 def test_master_ranks_and_gradient_match_reference(golden_dir):
     """NESMaster.compute_centered_ranks / gradient_estimate (nic_nes_master.py:170-221), imported by
     scripts/make_golden.py: P = 512. Tie-free fitness: ranks bit-exact. Tied fitness: the reference's
