@@ -535,7 +535,7 @@ def main():
         alg_bytes = step_noise_bytes_per_member(B) * P_local
     elif ph['step_launches']:
         # fused path: every step of a workgroup in one launch (nicnes_decode_steps_kernel), or one launch
-        # per step t = -1..T (nicnes_decode_step_kernel, DECODE_PERSISTENT=0 builds); coop path: the split
+        # per step t = -1..T (nicnes_decode_step_kernel, DECODE_PROF timing builds); coop path: the split
         # shape's every step in one launch (nicnes_decode_coop_kernel, S workgroups per member slab)
         if path == 'coop':
             kname = 'nicnes_decode_coop_kernel<%d>' % S_split

@@ -15,11 +15,12 @@
 // fp32(W0 +/- fp32(sigma * z[idx + offset])) from the base theta and the member's noise slice,
 // once for both signs.
 //
-// Step structure. One launch per step (nicnes_decode_step_kernel): the logit GEMM of step t over
-// h_t, the greedy token, then the LSTM cell of step t+1, whose gate sums i2h(x) + h2h(h)
-// (nets.py:109-111) use h_t while it is still the live B operand. The cell runs as 20 stages, one
-// per 32-unit gate tile (i2h rows | h2h rows), folded per unit block as the gates complete (order
-// g1, g2, i, f, o); only c' and h' cross to the next launch, in lane scratch.
+// Step structure (step_body; every step t = -1..T of a workgroup in one launch, nicnes_decode_steps_kernel):
+// the logit GEMM of step t over h_t, the greedy token, then the LSTM cell of step t+1, whose gate sums
+// i2h(x) + h2h(h) (nets.py:109-111) use h_t while it is still the live B operand. The cell runs as 20
+// stages, one per 32-unit gate tile (i2h rows | h2h rows), folded per unit block as the gates complete
+// (order g1, g2, i, f, o); only c' and h' cross to the next step, in lane scratch. Other paths: the coop
+// kernel (S workgroups per member slab in one launch), the 64-row-slab steps2 kernel, the split path.
 //
 // Addressing: every global access goes through a buffer resource (wave-uniform 128-bit
 // descriptor + 32-bit lane offset) so no 64-bit VGPR address pairs are kept live. Lane-derived
@@ -59,50 +60,12 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #ifndef NICNES_STORE_WAITS
 #define NICNES_STORE_WAITS 1  // the product: wait states after the sampled pick's 16-byte record stores (gfx950
 #endif                        // store-data hazard); 0 only in the scan's scratch build (tests/test_isa_hazards.py)
-#ifndef MFMA_FIRST_SIGN
-#define MFMA_FIRST_SIGN 0  // logit stages: the sign whose waves run the stage's MFMAs before the previous epilogue
-#endif
-#ifndef DECODE_FUSED2
-#define DECODE_FUSED2 1    // 64-row slabs with S = 1: every step in one launch (nicnes_decode_steps2_kernel)
-#endif
-#ifndef DECODE_PERSISTENT
-#define DECODE_PERSISTENT 1  // fused path: every step of a workgroup in one launch (0: one launch per step)
-#endif
-#ifndef IMG64
-#define IMG64 1            // fused path: image projection in 64-row stages with the fc chunk in registers
-#endif
-#ifndef CROSS_PREFETCH
-#define CROSS_PREFETCH 1   // steps kernel: a phase's first staging tile loaded during the previous phase's last stage
-#endif
-#ifndef H_PREFETCH
-#define H_PREFETCH 1      // steps kernel: h_{t+1} read back from lane scratch at the end of step t
-#endif
-#ifndef LOGIT_MIDSTORE
-#define LOGIT_MIDSTORE 1   // logit stages: the next stage's W+- tile is stored among the MFMAs of this one
-#endif
-#ifndef CELL_MIDSTORE
-#define CELL_MIDSTORE 1    // the steps kernel's cell stores tile m + 1 mid-way through tile m's MFMAs (-0.3 %, greedy)
-#endif
-#ifndef LOGIT_PEEL
-#define LOGIT_PEEL 1       // logit stages: the last two stages peeled off the stage loop (round 5: greedy steps kernel
-                           // -0.55 %, B = 64 steps2 -4.1 %; not kept for the coop (+1.4 %) and sampled (+2.2 %) decodes)
-#endif
-#ifndef LOGIT_MID_AT
-#define LOGIT_MID_AT 6     // ... before half-chunk LOGIT_MID_AT of 8 (measured: 5-7 equal, 2 and 8 -0.8 %)
-#endif
-#ifndef COOP_SC1
-#define COOP_SC1 0         // coop path: 1 = handed-off partials and h' read with sc1 loads instead of an agent acquire (measured: equal at P = 64, 0.6 % slower at P = 128)
-#endif
-#ifndef DECODE_PRIO
-#define DECODE_PRIO 0      // s_setprio 1 for one half of the workgroup's waves: 1 = waves 4-7, 2 = waves 0-3
-#endif
-__device__ __forceinline__ void wave_prio(int wave) {
-#if DECODE_PRIO == 1
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-#elif DECODE_PRIO == 2
-    if (wave < 4) __builtin_amdgcn_s_setprio(1);
-#endif
-}
+// The product's structural choices are fixed in the code below; each alternative was measured and dropped (DESIGN.md
+// sections 5 and 10 and the git history up to round 5): the other sign's waves first in the logit stages, one launch
+// per step, the 32-row-stage image projection on the fused path, no cross-phase prefetch / h read-back, the W+- store
+// at the end of a stage, other mid-stage store positions, the unpeeled stage loop in the greedy steps kernels, sc1 loads
+// of the coop hand-offs, s_setprio for half the waves, other cache policies of the sampled logit stores.
+#define LOGIT_MID_AT 6     // logit stages: the next stage's W+- tile is stored before half-chunk 6 of 8
 #ifndef DECODE_PROF
 #define DECODE_PROF 0      // timing-only build: per-workgroup start/end s_memrealtime (100 MHz) of every
 #endif                     // launch written over seq[wg * 4096 + slot] (wrong tokens; scripts/ablate.py)
@@ -151,10 +114,6 @@ __device__ __forceinline__ f32x4 ld4(rsrc_t r, uint32_t byte_off, uint32_t soff 
 }
 __device__ __forceinline__ float ld1(rsrc_t r, uint32_t byte_off, uint32_t soff = 0) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, (int)soff, 0));
-}
-// sc1 load (bypasses this CU's L1): a handed-off word read without an agent acquire (coop path)
-__device__ __forceinline__ float ld1_sc1(rsrc_t r, uint32_t byte_off, uint32_t soff = 0) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, (int)soff, 16));
 }
 __device__ __forceinline__ void st1(rsrc_t r, uint32_t byte_off, uint32_t soff, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)byte_off, (int)soff, 0);
@@ -389,7 +348,7 @@ struct NoMid {
 };
 
 // mid() runs before half-chunk MID of the 8 (8: after the last MFMA; 9: never): the logit loop's W+- store
-// of the next stage and the loads of the one after (LOGIT_MIDSTORE)
+// of the next stage and the loads of the one after
 template <int MID = 8, class Mid = NoMid>
 __device__ __forceinline__ void mfma_stage64_o(const float* w, const float* bias, const float (&Bop)[64], int arow,
                                                int hh, f32x16& acc0, f32x16& acc1, Mid&& mid = Mid()) {
@@ -766,13 +725,9 @@ __device__ __forceinline__ StageSrc logit_src(const DecodeParams& p, uint64_t ni
 // loads and then the crossing stage in one
 #define SLOG_BLOCK 8
 #define SLOG_BLK_BYTES 8192u
-#ifndef SAMP_L1_ROUND
 #define SAMP_L1_ROUND 20         // block records per round of the pick's level 1 (V1 <= 10240: one round)
-#endif
 #define SLOT_SPIN_TICKS 50000000ull   // 0.5 s of s_memrealtime (100 MHz) to find a free logit slot
-#ifndef SLOG_STORE_POLICY
 #define SLOG_STORE_POLICY 2      // cache policy of the slot stores: nt (streaming; -2 % sampled kernel time vs the default, measured)
-#endif
 
 __device__ __forceinline__ float samp_p(float x, float ref) {
     return __builtin_amdgcn_exp2f(__builtin_fmaf(x, LOG2E, -ref));
@@ -1045,7 +1000,7 @@ __device__ __forceinline__ void sample_pick(const DecodeParams& p, rsrc_t lr, ui
 
 // Measured and not kept (git history, r04): per-wave LDS progress words in place of the per-stage barrier (+0.4 %),
 // a chain-a-only last stage for the coop ranges (+1.3 % / +2.2 % at P = 64 / 128, or spills inside the loop).
-template <int G, bool PAIRS, bool PEEL = (LOGIT_PEEL != 0), class Tail = NoTail, class Hook = NoHook>
+template <int G, bool PAIRS, bool PEEL = true, class Tail = NoTail, class Hook = NoHook>
 __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, uint64_t nidx, int wave, int sgn,
                                              int hf, const float (&hB)[64], int s0, int s1, RowState& st,
                                              Stage64Regs& s64, bool preloaded = false, Tail&& tail = Tail(),
@@ -1067,30 +1022,25 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
     const bool bias = wave < 2;
     if (!preloaded) stage64_load_o(lsrc(s0), lo, bias, s64);
     stage64_store_o(lds, lsrc(s0).valid, lo, bias, s64);
-#if LOGIT_MIDSTORE
     // the registers carry stage s + 1 into stage s: its W+- tile is written before the last quarter of the
     // MFMAs of stage s (its buffer was last read in stage s - 1), then the loads of stage s + 2 are issued,
     // so the end of a stage has no staging wait and no LDS-write tail in front of the barrier
     if (PEEL) stage64_load_o(lsrc(min(s0 + 1, s1 - 1)), lo, bias, s64);   // (unconditional: one definition of s64)
     else if (s0 + 1 < s1) stage64_load_o(lsrc(s0 + 1), lo, bias, s64);
-#endif
     __syncthreads();
     f32x16 a0, a1, b0, b1;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { b0[r] = NEG_INF; b1[r] = NEG_INF; }
-    // MODE (LOGIT_PEEL): 0 a stage with two more after it (store s + 1, load s + 2), 1 the last but one (store
+    // MODE (PEEL): 0 a stage with two more after it (store s + 1, load s + 2), 1 the last but one (store
     // s + 1), 2 the last (the tail's loads); -1: decided at run time (the loop without the peel)
     auto stage = [&](auto mode_t, int s, f32x16& o0, f32x16& o1, const f32x16& q0, const f32x16& q1) {
         constexpr int MODE = decltype(mode_t)::value;
         const int sn = min(s + 1, s1 - 1);
-#if !LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
-        stage64_load_o(lsrc(sn), lo, bias, s64);
-#endif
         const float* buf = lds + ((s - s0) & 1) * STAGE64_FLOATS;
         const float* wsg = buf + sgn * (64 * LDS_ROW);
         const float* bsg = buf + 2 * 64 * LDS_ROW + 64 * sgn;
         auto mid = [&]() __attribute__((always_inline)) {
-#if LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
+#if !(DECODE_ABLATE & 2)
             // s64 is loaded on every non-last path (at s1 - 2 the load repeats tile s1 - 1): a conditional load
             // here would make the compiler copy the 32 staging registers at every stage to merge the paths
             if constexpr (MODE == 0) {
@@ -1108,9 +1058,9 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
             }
 #endif
         };
-        constexpr int MID = LOGIT_MIDSTORE ? LOGIT_MID_AT : 9;   // 9: never
+        constexpr int MID = LOGIT_MID_AT;
         if constexpr (G == 4) {
-            if (sgn == MFMA_FIRST_SIGN) {
+            if (sgn == 0) {
                 mfma_stage64_o<MID>(wsg, bsg, hB, lo.arow, hh, o0, o1, mid);
 #if !(DECODE_ABLATE & 1)
                 if constexpr (Hook::replaces) hook(q0, q1, s - 1);
@@ -1126,7 +1076,7 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
         } else {
             const float* w1 = wsg + 32 * hf * LDS_ROW;         // this wave's 32-row tile of the stage
             const float* bb = bsg + 32 * hf;
-            if (sgn == MFMA_FIRST_SIGN) {
+            if (sgn == 0) {
                 o0 = mfma_tile_o<MID>(bias_init(bb, hh), w1, hB, lo.arow, mid);
                 epilogue32<PAIRS>(st, q0, 64 * (s - 1) + vl);
             } else {
@@ -1134,9 +1084,6 @@ __device__ __forceinline__ void logit_stages(float* lds, const DecodeParams& p, 
                 o0 = mfma_tile_o<MID>(bias_init(bb, hh), w1, hB, lo.arow, mid);
             }
         }
-#if !LOGIT_MIDSTORE && !(DECODE_ABLATE & 2)
-        stage64_store_o(lds + ((s - s0 + 1) & 1) * STAGE64_FLOATS, lsrc(sn).valid, lo, bias, s64);
-#endif
 #if !(DECODE_ABLATE & 8)
         __syncthreads();
 #endif
@@ -1488,7 +1435,7 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         row_state_init(st);
         // the cell's first gate tile does not depend on the token: its loads are issued at the last logit
         // stage's mid-point (tail) and land while the token is picked
-        const bool xpre = CROSS_PREFETCH && t < p.T;
+        const bool xpre = t < p.T;
         auto tail = [&]() __attribute__((always_inline)) {
             if (xpre) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
         };
@@ -1500,11 +1447,11 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
                                  16u * (uint32_t)lane_fresh() + 1024u * (uint32_t)c.wave, (p.V1 + 63) >> 6, sm, sref, sT,
                                  sB};
             // (no peel for the sampled decode: +2.2 %, measured)
-            logit_stages<4, PAIRS, false>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail, ss);
+            logit_stages<4, PAIRS, false>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre, tail, ss);
         } else {
-            logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre && LOGIT_MIDSTORE, tail);
+            logit_stages<4, PAIRS>(lds, p, nidx, c.wave, c.sgn, 0, hB, 0, nl, st, s64, pre, tail);
         }
-        cell_pre = xpre && LOGIT_MIDSTORE;
+        cell_pre = xpre;
         PROF_MARK(120 + 24 * (t + 1));
 
         // ---- greedy token (nets.py:208-209) ------------------------------------------------
@@ -1623,7 +1570,7 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
     PROF_MARK(120 + 24 * (t + 1) + 1);
     if (!cell_pre) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
     stage64_store(lds + b0 * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
-    constexpr bool CMID = CELL_MIDSTORE && !SAMPLE;              // (the sampled decode: +0.9 %, measured)
+    constexpr bool CMID = !SAMPLE;                               // (the sampled decode: +0.9 %, measured)
     if constexpr (CMID) stage64_load(csrc(1), c.wave * 64 + lane_fresh(), s64);   // tile 1: stored at tile 0's mid-point
     __syncthreads();
     f32x16 hold;
@@ -1713,7 +1660,7 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
         PROF_MARK(120 + 24 * (t + 1) + 2 + m);
     }
     pre = PREFETCH && t >= 0;
-    if (PREFETCH && H_PREFETCH && t + 1 <= p.T) {                // h_{t+1}: this lane's own h' stores, read back
+    if (PREFETCH && t + 1 <= p.T) {                // h_{t+1}: this lane's own h' stores, read back
 #pragma unroll                                                  // while the next step's prologue runs
         for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, H_SLOT(i));
         hpre = true;
@@ -1722,17 +1669,19 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
     return true;
 }
 
+#if DECODE_PROF
+// timing build only: one launch per step t, so the marks of every workgroup and step land in its own seq slots
 template <bool PAIRS>
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodeParams p, int t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const Ctx c = make_ctx(p);
     if (t > 0 && p.alive[c.wg] == 0) return;
-    wave_prio(c.wave);
     Stage64Regs s64;
     bool pre = false, hpre = false;
     float hB[64];
     step_body<PAIRS, false>(p, c, lds, t, s64, pre, hB, hpre);
 }
+#endif
 
 // The whole decode of a workgroup (steps t = -1 .. T) in one launch: a member's steps depend only on
 // that member, so nothing needs a grid-wide step boundary. Saves the per-launch ramp and tail (every
@@ -1774,12 +1723,11 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodePar
         c.slog_r = make_rsrc(p.slog + (size_t)slot * (sbytes / 4), sbytes);
         static_assert(SLOG_STAGE_BYTES % 4 == 0, "slot stage size");
     }
-    wave_prio(c.wave);
     Stage64Regs s64;
     bool pre = false, hpre = false;
     float hB[64];
     for (int t = -1; t <= p.T; ++t)
-        if (!step_body<PAIRS, LOGIT_MIDSTORE && CROSS_PREFETCH, SAMPLE>(p, c, lds, t, s64, pre, hB, hpre)) break;
+        if (!step_body<PAIRS, true, SAMPLE>(p, c, lds, t, s64, pre, hB, hpre)) break;
     if constexpr (SAMPLE) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's accesses of the slot are done
         __syncthreads();
@@ -2235,11 +2183,11 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         RowState st;
         row_state_init(st);
         auto tail = [&]() __attribute__((always_inline)) {
-            if (CROSS_PREFETCH && t < p.T) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
+            if (t < p.T) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
         };
         // (no peel here: +1.4 % at P = 64, the coop kernel's spills 28 -> 80)
-        logit_stages<4, PAIRS, false>(lds, p, nidx, c.wave, c.sgn, 0, hB, s0, s1, st, s64, pre && LOGIT_MIDSTORE, tail);
-        cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && t < p.T;
+        logit_stages<4, PAIRS, false>(lds, p, nidx, c.wave, c.sgn, 0, hB, s0, s1, st, s64, pre, tail);
+        cell_pre = t < p.T;
         PROF_AT(blockIdx.x, 1024, pm + 1);
         // ---- phase A: this range's partial greedy state, write-through, then the group's merge
         {
@@ -2256,7 +2204,7 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         coop_arrive(ctr);
         ++phase;
 #if !(DECODE_ABLATE & 128)
-        if (!coop_wait<!COOP_SC1>(ctr, (uint32_t)S * phase, p.stats)) return false;
+        if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
 #endif
         PROF_AT(blockIdx.x, 1024, pm + 2);
         float m = 0.f, lse = 0.f;
@@ -2264,32 +2212,10 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         bool ovf = false;
         {
             Part8 pr;
-#if COOP_SC1
-            {   // the S partial states of this wave's rows, sc1 loads (written sc1 by the group)
-                const uint32_t po = 4u * (uint32_t)(c.wave * (7 * 64) + lane_fresh());
-#pragma unroll
-                for (int u = 0; u < S; ++u) {
-                    const rsrc_t r = make_rsrc(part_ptr(p, c.wg, u, 0), PART_FLOATS * 4);
-                    pr.m[u] = ld1_sc1(r, po, 0u); pr.s[u] = ld1_sc1(r, po, 256u);
-                    pr.r0v[u] = ld1_sc1(r, po, 512u); pr.r0i[u] = __builtin_bit_cast(int, ld1_sc1(r, po, 768u));
-                    pr.r1v[u] = ld1_sc1(r, po, 1024u); pr.r1i[u] = __builtin_bit_cast(int, ld1_sc1(r, po, 1280u));
-                    pr.ev[u] = ld1_sc1(r, po, 1536u);
-                }
-            }
-#else
             load_part8(p, c.wg, c.wave, lane_fresh(), 1, S, 0, pr);
-#endif
             merge_partials(p, c.wg, c.wave, lane_fresh(), 1, S, pr, PAIRS, m, lse, tok, ovf);
         }
         if (__syncthreads_or((p.force_exact || ovf) ? 1 : 0)) {
-#if COOP_SC1
-            // the exact pass re-reads the partials with plain loads: acquire them first (rare path)
-            if (threadIdx.x < 64) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();
-#endif
             // the exact sweep stages through LDS with registers of its own: the prefetched cell tile is
             // given up (reloaded below)
             merge_exact(p, lds, c.wg, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.wave, c.lane, 1, S, hB, true,
@@ -2371,7 +2297,7 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
         for (int r = 0; r < 16; ++r) cp[r] = (m % 5 == 3 && t >= 0) ? ld1(c.scr_r, lo_, C_SLOT(16 * (m / 5) + r)) : 0.f;
         return cp;
     };
-    const bool lpf = LOGIT_MIDSTORE && CROSS_PREFETCH && t >= 0;   // the next step's first logit tile
+    const bool lpf = t >= 0;                                       // the next step's first logit tile
 #pragma unroll 1
     for (int m = m0; m < m1; ++m) {
         const f32x16 cpre = load_c(m);
@@ -2398,11 +2324,11 @@ __device__ __forceinline__ bool coop_step(const DecodeParams& p, const Ctx& c, i
     coop_arrive(ctr);
     ++phase;
 #if !(DECODE_ABLATE & 128)
-    if (!coop_wait<!COOP_SC1>(ctr, (uint32_t)S * phase, p.stats)) return false;
+    if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
 #endif
     PROF_AT(blockIdx.x, 1024, pm + 5);
 #pragma unroll
-    for (int i = 0; i < 64; ++i) hB[i] = COOP_SC1 ? ld1_sc1(c.scr_r, lo, HP_SLOT(hpar, i)) : ld1(c.scr_r, lo, HP_SLOT(hpar, i));
+    for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, HP_SLOT(hpar, i));
     return true;
 }
 
@@ -2489,10 +2415,10 @@ __device__ __forceinline__ bool step_body2(const DecodeParams& p, const SCtx<2>&
         RowState st;
         row_state_init(st);
         auto tail = [&]() __attribute__((always_inline)) {
-            if (CROSS_PREFETCH && t < p.T) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
+            if (t < p.T) stage64_load(csrc(0), c.wave * 64 + lane_fresh(), s64);
         };
-        logit_stages<2, PAIRS>(lds, p, nidx, c.wave, c.sgn, c.hf, hB, 0, nst, st, s64, pre && LOGIT_MIDSTORE, tail);
-        cell_pre = CROSS_PREFETCH && LOGIT_MIDSTORE && t < p.T;
+        logit_stages<2, PAIRS>(lds, p, nidx, c.wave, c.sgn, c.hf, hB, 0, nst, st, s64, pre, tail);
+        cell_pre = t < p.T;
         {   // this tile half's partial greedy state (read back by the half-0 wave of the row group)
             float* pb = part_ptr(p, c.wg, 0, c.wave) + lane_fresh();
             pb[0] = st.m;
@@ -2597,7 +2523,7 @@ __device__ __forceinline__ bool step_body2(const DecodeParams& p, const SCtx<2>&
         return cp;
     };
     float* xch = lds + 2 * STAGE64_FLOATS + (c.sgn * 2 + c.grp) * 1024;   // h2h half -> i2h half
-    const bool lpf = LOGIT_MIDSTORE && CROSS_PREFETCH && t >= 0;          // the next step's first logit tile
+    const bool lpf = t >= 0;                                              // the next step's first logit tile
 #pragma unroll 1
     for (int m = 0; m < 20; ++m) {
         const f32x16 cpre = load_c(m);
@@ -2658,8 +2584,10 @@ const size_t LDS_CELL2 = LDS64 + (size_t)4 * 1024 * sizeof(float);   // + the G 
 // per device, once per handle (nicnes_create, after hipSetDevice): dynamic LDS above 64 KB
 extern "C" hipError_t nicnes_decode_init() {
     const struct { const void* f; size_t b; } ks[] = {
+#if DECODE_PROF
         {(const void*)nicnes_decode_step_kernel<true>, LDS64},
         {(const void*)nicnes_decode_step_kernel<false>, LDS64},
+#endif
         {(const void*)nicnes_decode_img64_kernel, LDS64},
         {(const void*)nicnes_decode_steps_kernel<true>, LDS64},
         {(const void*)nicnes_decode_steps_kernel<false>, LDS64},
@@ -2759,22 +2687,20 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
         if (e != hipSuccess) return e;
         mark(DK_COOP);
     } else if (fused) {
-        if (IMG64)
-            hipLaunchKernelGGL(nicnes_decode_img64_kernel, dim3(member_count, nslabs), block, LDS64, stream, *p);
-        else
-            hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(1, member_count, nslabs), block, LDS32, stream, *p);
+        hipLaunchKernelGGL(nicnes_decode_img64_kernel, dim3(member_count, nslabs), block, LDS64, stream, *p);
         mark(DK_IMG);
         const dim3 grid(member_count, nslabs);
         if (p->sample_u) {                                  // sampled decode: the exact lse, then the draw's pick
             hipLaunchKernelGGL((nicnes_decode_steps_kernel<false, true>), grid, block, LDS64, stream, *p);
             mark(DK_STEPS);
-        } else if (DECODE_PERSISTENT && !DECODE_PROF) {
+        } else {
+#if !DECODE_PROF
             if (pairs)
                 hipLaunchKernelGGL(nicnes_decode_steps_kernel<true>, grid, block, LDS64, stream, *p);
             else
                 hipLaunchKernelGGL(nicnes_decode_steps_kernel<false>, grid, block, LDS64, stream, *p);
             mark(DK_STEPS);
-        } else {
+#else
             for (int t = -1; t <= p->T; ++t) {
                 if (pairs)
                     hipLaunchKernelGGL(nicnes_decode_step_kernel<true>, grid, block, LDS64, stream, *p, t);
@@ -2782,6 +2708,7 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
                     hipLaunchKernelGGL(nicnes_decode_step_kernel<false>, grid, block, LDS64, stream, *p, t);
                 mark(DK_STEP);
             }
+#endif
         }
     } else {
         const int Sc = p->S < 4 ? p->S : 4;
@@ -2800,7 +2727,7 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
                 hipLaunchKernelGGL(nicnes_decode_cell_kernel<4>, gc, block, LDS64, stream, *p, t);
                 mark(DK_CELL);
             }
-        } else if (p->S == 1 && DECODE_FUSED2 && !DECODE_PROF) {
+        } else if (p->S == 1 && !DECODE_PROF) {
             // 64-row slabs, one workgroup per member slab: every step in one launch
             hipLaunchKernelGGL(nicnes_decode_img_kernel<2>, gc, block, LDS32, stream, *p);
             mark(DK_IMG);

@@ -361,7 +361,7 @@ class Engine:
     def decode_phase_times(self):
         """Per-kernel split of the last timed decode (HIP events between its launches): img_ms,
         step_ms / step_launches (fused path: the steps kernel, every step t = -1..T in one launch; one
-        launch per step in DECODE_PERSISTENT=0 builds, whose first two, cell-only, launches are also in
+        launch per step in DECODE_PROF timing builds, whose first two, cell-only, launches are also in
         cell_only_ms), logit_ms / logit_launches and cell_ms / cell_launches (split path)."""
         out = (ctypes.c_float * 8)()
         check(self.L.nicnes_decode_phase_times(self.h, out), self.h, 'decode_phase_times')
