@@ -113,9 +113,36 @@ def kernel_source_sha256():
     return h.hexdigest()
 
 
-def load_pmc(kernel, P, B):
-    """The newest committed PMC profile of (kernel, members per GPU, B) whose recorded source hash is
-    the current one; (None, reason) when there is none (stale counters are never reported)."""
+# the instantiation a PMC key names: (key, PAIRS) -> mangled symbol (PAIRS: the greedy-only bounded-lse variant)
+PMC_SYMBOLS = {
+    ('steps', True): '_Z26nicnes_decode_steps_kernelILb1ELb0EEv12DecodeParams',
+    ('steps', False): '_Z26nicnes_decode_steps_kernelILb0ELb0EEv12DecodeParams',
+    ('sampled', False): '_Z26nicnes_decode_steps_kernelILb0ELb1EEv12DecodeParams',
+    ('coop4', True): '_Z25nicnes_decode_coop_kernelILb1ELi4EEv12DecodeParamsi',
+    ('coop4', False): '_Z25nicnes_decode_coop_kernelILb0ELi4EEv12DecodeParamsi',
+    ('coop2', True): '_Z25nicnes_decode_coop_kernelILb1ELi2EEv12DecodeParamsi',
+    ('coop2', False): '_Z25nicnes_decode_coop_kernelILb0ELi2EEv12DecodeParamsi',
+    ('steps2', True): '_Z27nicnes_decode_steps2_kernelILb1EEv12DecodeParams',
+    ('steps2', False): '_Z27nicnes_decode_steps2_kernelILb0EEv12DecodeParams',
+    ('logit', True): '_Z26nicnes_decode_logit_kernelILi4ELb1EEv12DecodeParamsi',
+    ('logit', False): '_Z26nicnes_decode_logit_kernelILi4ELb0EEv12DecodeParamsi',
+}
+LIBRARY = os.path.join(REPO, 'nes-img-captioning_amd', 'nicnes', 'libnicnes.so')
+_listings = {}
+
+
+def library_kernel_sha(symbol, library=LIBRARY):
+    """SHA-256 of the symbol's machine code in the library this run loads (nicnes.codeobj)."""
+    from nicnes import codeobj
+    if library not in _listings:
+        _listings[library] = codeobj.kernel_listings(library)
+    return codeobj.kernel_isa_sha256(library, symbol, _listings[library])
+
+
+def load_pmc(kernel, P, B, pairs=True):
+    """The newest committed PMC profile of (kernel, members per GPU, B) measured on the machine code the library
+    holds now for that kernel instantiation (its kernel_isa_sha256; profiles without one: the decode sources'
+    hash); (None, reason) when there is none (stale counters are never reported)."""
     import glob
     key = PMC_KEYS.get(kernel)
     if key is None:
@@ -123,15 +150,22 @@ def load_pmc(kernel, P, B):
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_%s_p%d_b%d.json' % (key, P, B))), reverse=True)
     if not files:
         return None, None
+    symbol = PMC_SYMBOLS.get((key, pairs if key != 'sampled' else False))
     sha = kernel_source_sha256()
     for f in files:
         with open(f) as fh:
             rec = json.load(fh)
-        if rec.get('source_sha256') == sha:
+        if rec.get('kernel_isa_sha256'):
+            ok = rec.get('kernel_symbol') == symbol and library_kernel_sha(symbol) == rec['kernel_isa_sha256']
+        else:
+            ok = rec.get('source_sha256') == sha
+        if ok:
             rec['file'] = os.path.relpath(f, REPO)
             return rec, None
-    reason = ('%s records kernel source %s, the tree has %s: counters not reported (re-run the PMC passes)'
-              % (os.path.relpath(files[0], REPO), str(rec.get('source_sha256'))[:12], sha[:12]))
+    reason = ('%s measured %s (machine code %s / source %s); the library holds %s: counters not reported (re-run the '
+              'PMC passes)' % (os.path.relpath(files[0], REPO), rec.get('kernel_symbol'),
+                               str(rec.get('kernel_isa_sha256'))[:12], str(rec.get('source_sha256'))[:12],
+                               str(library_kernel_sha(symbol) if symbol else None)[:12]))
     print('bench.py: STALE PMC PROFILE: ' + reason, file=sys.stderr, flush=True)
     return None, reason
 
@@ -555,7 +589,10 @@ def main():
     achieved = step_flop / (step_ms / 1e3) / 1e12
     # counter figures of the same kernel and workload from the committed rocprofv3 PMC profile
     # (a profile-derived constant: PMC passes cannot run inside the timed bench process)
-    pmc, pmc_stale = load_pmc(kname, P_local, B)
+    # (the greedy-only bounded-lse instantiation unless log-probs are written or NICNES_BOUNDED_LSE=0; the engine's
+    # adaptive policy may run some decodes of a peaked theta on the exact one)
+    pairs_run = args.fitness == 'greedy' and os.environ.get('NICNES_BOUNDED_LSE', '2') != '0'
+    pmc, pmc_stale = load_pmc(kname, P_local, B, pairs_run)
     traffic = pmc['derived'].get('hbm_bytes_per_launch') if pmc else None
     hbm_peak_bytes = HBM_PEAK_GBS * 1e9 * step_ms / 1e3
     iter_bytes = iteration_algorithmic_bytes(B, P_local)
@@ -596,6 +633,7 @@ def main():
                      'algorithmic_bytes_per_launch': alg_bytes,
                      'traffic_over_algorithmic': (round(traffic / alg_bytes, 3) if traffic else None),
                      'traffic_source': pmc['file'] if pmc else None,
+                     'traffic_kernel_symbol': pmc.get('kernel_symbol') if pmc else None,
                      'traffic_stale': pmc_stale,
                      'hbm_frac': round(alg_bytes / hbm_peak_bytes, 4),
                      'hbm_frac_counters': round(traffic / hbm_peak_bytes, 4) if traffic else None,

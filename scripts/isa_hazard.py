@@ -33,36 +33,8 @@ _FUNC = re.compile(r'^[0-9a-f]+ <(.+)>:$')
 _INSN = re.compile(r'^\s+([a-z_0-9]+)(?:\s+(.*?))?\s*(?://.*)?$')
 
 
-def code_objects(so_path):
-    """The gfx950 code objects of every offload bundle in the library's .hip_fatbin section."""
-    with tempfile.TemporaryDirectory() as td:
-        fb = os.path.join(td, 'fatbin')
-        subprocess.check_call([os.path.join(LLVM, 'llvm-objcopy'), '--dump-section', '.hip_fatbin=' + fb, so_path,
-                               os.path.join(td, 'lib.so')])
-        with open(fb, 'rb') as f:
-            data = f.read()
-    out = []
-    start = data.find(BUNDLE_MAGIC)
-    while start >= 0:
-        n = struct.unpack_from('<Q', data, start + len(BUNDLE_MAGIC))[0]
-        p = start + len(BUNDLE_MAGIC) + 8
-        for _ in range(n):
-            off, size, tlen = struct.unpack_from('<QQQ', data, p)
-            p += 24
-            triple = data[p:p + tlen].decode()
-            p += tlen
-            if triple.endswith('--' + ARCH) and size:
-                out.append((triple, data[start + off:start + off + size]))
-        start = data.find(BUNDLE_MAGIC, start + 1)
-    return out
-
-
-def disassemble(code):
-    with tempfile.NamedTemporaryFile(suffix='.co') as f:
-        f.write(code)
-        f.flush()
-        return subprocess.check_output([os.path.join(LLVM, 'llvm-objdump'), '-d', '--mcpu=' + ARCH, f.name],
-                                       text=True)
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'nes-img-captioning_amd'))
+from nicnes.codeobj import code_objects, disassemble  # noqa: E402,F401  (the library's gfx950 code objects)
 
 
 def vregs(tok):

@@ -1,11 +1,13 @@
 """Turn one profile.sh run (gpurun_out/<TAG>/) into the committed profile files (dev tool):
   profiles/<round>_kernel_stats_p<P>.csv       rocprofv3 --kernel-trace --stats summary of the bench
   profiles/<round>_decode_launches_p<P>.json   full-population launch averages (scripts/trace_summary.py)
-  profiles/<round>_pmc_<key>_p<P>_b128.json    per-launch PMC counters + derived figures (pmc_summary.py),
-                                               stamped with the decode sources' hash (bench.py reads it)
+  profiles/<round>_pmc_<key>_p<P>_b<B>.json    per-launch PMC counters + derived figures (pmc_summary.py),
+                                               stamped with the measured instantiation's machine-code hash in
+                                               the tree's library (bench.py load_pmc checks it)
   profiles/<round>_bench_profiled_p<P>.json    the bench line printed under the profiler
-P = members per GPU: 512 -> the fused steps kernel, 128 / 64 -> the coop kernel (S = 2 / 4).
-usage: python scripts/make_profiles.py TAG [ROUND] [P ...]
+P = members per GPU: 512 / 256 -> the fused steps kernel, 128 / 64 -> the coop kernel (S = 2 / 4); P:b64 -> the
+64-row-slab steps2 kernel (a profile.sh run with --batch 64), P:sampled -> the sampled steps kernel (--fitness sample).
+usage: python scripts/make_profiles.py TAG [ROUND] [P[:b64|:sampled] ...]
 """
 import json
 import os
@@ -19,25 +21,35 @@ import bench  # noqa: E402
 
 tag = sys.argv[1]
 rnd = sys.argv[2] if len(sys.argv) > 2 else 'r03'
-pops = [int(x) for x in sys.argv[3:]] or [512, 128, 64]
+pops = sys.argv[3:] or ['512', '128', '64']
 src = os.path.join(REPO, 'gpurun_out', tag)
 out = os.path.join(REPO, 'profiles')
-B = 128
 KERNELS = {512: ('steps', 'nicnes_decode_steps_kernel'), 256: ('steps', 'nicnes_decode_steps_kernel'),
            128: ('coop2', 'nicnes_decode_coop_kernel<true, 2>'), 64: ('coop4', 'nicnes_decode_coop_kernel<true, 4>')}
-for P in pops:
-    key, kernel = KERNELS[P]
+for tok in pops:
+    P, mode = (int(tok.split(':')[0]), tok.split(':')[1] if ':' in tok else '')
+    B = 64 if mode == 'b64' else 128
+    key, kernel = {'': KERNELS.get(P), 'b64': ('steps2', 'nicnes_decode_steps2_kernel<true>'),
+                   'sampled': ('sampled', 'nicnes_decode_steps_kernel<false, true>')}[mode]
+    rows = 5 * B if mode == 'sampled' else B
     st = os.path.join(src, 'stats%d' % P)
-    shutil.copy(os.path.join(st, 'run_kernel_stats.csv'), os.path.join(out, '%s_kernel_stats_p%d.csv' % (rnd, P)))
-    launches = os.path.join(out, '%s_decode_launches_p%d.json' % (rnd, P))
+    sfx = '' if not mode else '_' + mode
+    shutil.copy(os.path.join(st, 'run_kernel_stats.csv'), os.path.join(out, '%s_kernel_stats_p%d%s.csv' % (rnd, P, sfx)))
+    launches = os.path.join(out, '%s_decode_launches_p%d%s.json' % (rnd, P, sfx))
     subprocess.check_call([sys.executable, os.path.join(REPO, 'scripts', 'trace_summary.py'), '--trace', st,
                            '--out', launches, '--command', 'python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline '
                            '--population %d' % P], stdout=subprocess.DEVNULL)
     with open(launches) as f:
         lj = json.load(f)
-    rec = [v for k, v in lj['kernels'].items() if kernel.split('<')[0] in k][0]
+    recs = [v for k, v in lj['kernels'].items() if kernel in k] or \
+        [v for k, v in lj['kernels'].items() if kernel.split('<')[0] in k]
+    rec = max(recs, key=lambda v: v['mean_ms_full_grid'])     # (the workload setup's one-member decode is not it)
     dur_ms = rec['mean_ms_full_grid']
-    if key in ('step', 'steps', 'coop2', 'coop4'):
+    if key == 'sampled':                                 # + the slot writes (bench.py's sampled accounting)
+        nst = (9488 + 63) // 64
+        flop = bench.step_flops_per_member(rows) * P
+        alg = (bench.step_noise_bytes_per_member(rows) + 16 * (rows // 128) * (nst * 73728 + (nst + 7) // 8 * 8192)) * P
+    elif key in ('step', 'steps', 'coop2', 'coop4', 'steps2'):
         n_launch = 18 if key == 'step' else 1           # one launch per step, or every step in one launch
         flop = bench.step_flops_per_member(B) * P / n_launch
         alg = bench.step_noise_bytes_per_member(B) * P / n_launch
@@ -48,14 +60,17 @@ for P in pops:
     for i in range(4):
         passes += ['--pass', os.path.join(src, 'pmc%d_%d' % (P, i))]
     pmc = os.path.join(out, '%s_pmc_%s_p%d_b%d.json' % (rnd, key, P, B))
+    symbol = bench.PMC_SYMBOLS[(key, mode != 'sampled')]
     subprocess.check_call([sys.executable, os.path.join(REPO, 'scripts', 'pmc_summary.py'), '--kernel',
-                           kernel.split('<')[0]] + passes +
+                           kernel.split('<')[0], '--symbol', symbol] + passes +
                           ['--duration-ms', '%.6f' % dur_ms, '--algorithmic-bytes', str(alg), '--algorithmic-flop',
                            str(flop), '--note', 'bench.py --population %d (B=128), rocprofv3 --pmc passes of %s; '
-                           'duration = full-grid launch average of the kernel-trace run' % (P, tag), '--out', pmc])
+                           'duration = full-grid launch average of the kernel-trace run' % (P, tag) +
+                           (', --batch 64' if mode == 'b64' else ', --fitness sample' if mode == 'sampled' else ''),
+                           '--out', pmc])
     with open(os.path.join(src, 'stats%d.log' % P)) as f:
         lines = [l for l in f.read().splitlines() if l.startswith('{"metric"')]
     if lines:
-        with open(os.path.join(out, '%s_bench_profiled_p%d.json' % (rnd, P)), 'w') as f:
+        with open(os.path.join(out, '%s_bench_profiled_p%d%s.json' % (rnd, P, sfx)), 'w') as f:
             f.write(lines[-1] + '\n')
     print(P, kernel, 'avg ms', round(dur_ms, 4), 'TF/s', round(flop / dur_ms / 1e9, 2))

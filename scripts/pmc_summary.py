@@ -60,6 +60,8 @@ def main():
     ap.add_argument('--algorithmic-bytes', type=float, default=None)
     ap.add_argument('--algorithmic-flop', type=float, default=None)
     ap.add_argument('--note', default='')
+    ap.add_argument('--symbol', default=None, help='mangled name of the measured instantiation: the profile records '
+                    'its machine-code hash in the tree\'s library (bench.load_pmc checks it)')
     ap.add_argument('--out', required=True)
     a = ap.parse_args()
     counters, dispatches = {}, {}
@@ -70,6 +72,9 @@ def main():
     c = counters
     out = {'kernel': a.kernel, 'note': a.note, 'source_sha256': bench.kernel_source_sha256(),
            'counters_per_launch': c, 'dispatches': dispatches}
+    if a.symbol:
+        out['kernel_symbol'] = a.symbol
+        out['kernel_isa_sha256'] = bench.library_kernel_sha(a.symbol)
     d = {}
     if 'FETCH_SIZE' in c and 'WRITE_SIZE' in c:
         d['hbm_bytes_per_launch'] = (2.0 * c['FETCH_SIZE'] + c['WRITE_SIZE']) * 1024.0

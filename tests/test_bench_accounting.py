@@ -61,7 +61,8 @@ def test_presets_name_the_baseline_configs():
 def test_committed_pmc_profiles_match_the_decode_sources():
     """The bench line's counter figures (traffic, MFMA busy) come from committed PMC profiles: every shape the
     bench reports (the fused kernel at 512 and 256 members per GPU, the coop kernel at 128 and 64, the sampled
-    kernel) has one recorded against the current decode sources."""
+    kernel) has one measured on the machine code the built library holds now for that instantiation (round 6:
+    kernel_isa_sha256 of the symbol, nicnes.codeobj; a source edit that leaves the instructions unchanged keeps it)."""
     for kernel, P in (('nicnes_decode_steps_kernel', 512), ('nicnes_decode_coop_kernel<2>', 128),
                       ('nicnes_decode_coop_kernel<4>', 64), ('nicnes_decode_steps_kernel<sample>', 512)):
         rec, why = bench.load_pmc(kernel, P, 128)
