@@ -1155,6 +1155,11 @@ __device__ __forceinline__ bool row_ok(const DecodeParams& p, int b, int sgn) {
     return b < p.B && b + sgn * p.sign_off < p.B_img * p.rpi;
 }
 
+// XCD_GROUP (the sampled decode, whose rollouts span several 128-row slabs): the member slabs are taken in groups of
+// 8 members, slab-major inside a group, so the slabs of one member are dispatched next to each other and, with the
+// dispatcher's round-robin over the 8 XCDs (linear block id mod 8), on the same XCD: the member's noise rows are then
+// read from HBM by one slab and from that XCD's L2 by the others, instead of once per slab a whole grid apart.
+template <bool XCD_GROUP = false>
 __device__ __forceinline__ Ctx make_ctx(const DecodeParams& p) {
     Ctx c;
     c.tid = threadIdx.x;
@@ -1165,6 +1170,13 @@ __device__ __forceinline__ Ctx make_ctx(const DecodeParams& p) {
     c.hh = c.lane >> 5;
     c.member = blockIdx.x;
     c.slab = blockIdx.y;
+    if constexpr (XCD_GROUP) {
+        const int M = (int)gridDim.x, NS = (int)gridDim.y;
+        const int L = (int)(blockIdx.x + gridDim.x * blockIdx.y), gs = 8 * NS, g = L / gs;
+        const int w = min(8, M - 8 * g), r = L - g * gs;       // members in this group (the last may hold fewer)
+        c.member = 8 * g + r % w;
+        c.slab = r / w;
+    }
     c.wg = c.member * gridDim.y + c.slab;
     c.b = c.slab * 128 + c.grp * 32 + (c.lane & 31);
     c.row_valid = row_ok(p, c.b, c.sgn);
@@ -1695,7 +1707,7 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_step_kernel(DecodePara
 template <bool PAIRS, bool SAMPLE = false>
 __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodeParams p) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    Ctx c = make_ctx(p);
+    Ctx c = make_ctx<SAMPLE>(p);
     int slot = -1;
     if constexpr (SAMPLE) {
         __shared__ int slot_sh;
