@@ -6,7 +6,8 @@
                                                the tree's library (bench.py load_pmc checks it)
   profiles/<round>_bench_profiled_p<P>.json    the bench line printed under the profiler
 P = members per GPU: 512 / 256 -> the fused steps kernel, 128 / 64 -> the coop kernel (S = 2 / 4); P:b64 -> the
-64-row-slab steps2 kernel (a profile.sh run with --batch 64), P:sampled -> the sampled steps kernel (--fitness sample).
+64-row-slab steps2 kernel (a profile.sh run with --batch 64), P:sampled -> the sampled steps kernel (--fitness sample),
+P:trained -> the steps kernel on the trained-like theta (--theta-gain 4 --bias-std 0.1; key steps-trained).
 usage: python scripts/make_profiles.py TAG [ROUND] [P[:b64|:sampled] ...]
 """
 import json
@@ -30,7 +31,8 @@ for tok in pops:
     P, mode = (int(tok.split(':')[0]), tok.split(':')[1] if ':' in tok else '')
     B = 64 if mode == 'b64' else 128
     key, kernel = {'': KERNELS.get(P), 'b64': ('steps2', 'nicnes_decode_steps2_kernel<true>'),
-                   'sampled': ('sampled', 'nicnes_decode_steps_kernel<false, true>')}[mode]
+                   'sampled': ('sampled', 'nicnes_decode_steps_kernel<false, true>'),
+                   'trained': ('steps', 'nicnes_decode_steps_kernel<false, false>')}[mode]
     rows = 5 * B if mode == 'sampled' else B
     st = os.path.join(src, 'stats%d' % P)
     sfx = '' if not mode else '_' + mode
@@ -59,14 +61,17 @@ for tok in pops:
     passes = []
     for i in range(4):
         passes += ['--pass', os.path.join(src, 'pmc%d_%d' % (P, i))]
-    pmc = os.path.join(out, '%s_pmc_%s_p%d_b%d.json' % (rnd, key, P, B))
-    symbol = bench.PMC_SYMBOLS[(key, mode != 'sampled')]
+    pmc = os.path.join(out, '%s_pmc_%s_p%d_b%d.json' % (rnd, key + ('-trained' if mode == 'trained' else ''), P, B))
+    # (trained: the peaked theta of --theta-gain 4 --bias-std 0.1, where the engine's adaptive policy runs the exact-lse
+    # instantiation; its profile is kept under its own key so the bench's default line never reads it)
+    symbol = bench.PMC_SYMBOLS[(key, mode not in ('sampled', 'trained'))]
     subprocess.check_call([sys.executable, os.path.join(REPO, 'scripts', 'pmc_summary.py'), '--kernel',
                            kernel.split('<')[0], '--symbol', symbol] + passes +
                           ['--duration-ms', '%.6f' % dur_ms, '--algorithmic-bytes', str(alg), '--algorithmic-flop',
                            str(flop), '--note', 'bench.py --population %d (B=128), rocprofv3 --pmc passes of %s; '
                            'duration = full-grid launch average of the kernel-trace run' % (P, tag) +
-                           (', --batch 64' if mode == 'b64' else ', --fitness sample' if mode == 'sampled' else ''),
+                           {'b64': ', --batch 64', 'sampled': ', --fitness sample',
+                            'trained': ', --theta-gain 4 --bias-std 0.1'}.get(mode, ''),
                            '--out', pmc])
     with open(os.path.join(src, 'stats%d.log' % P)) as f:
         lines = [l for l in f.read().splitlines() if l.startswith('{"metric"')]
