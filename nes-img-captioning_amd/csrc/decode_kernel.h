@@ -51,6 +51,18 @@ struct DecodeParams {
     int64_t off_img_w, off_img_b, off_emb_w, off_log_w, off_log_b, off_i2h_w, off_i2h_b, off_h2h_w, off_h2h_b;
 };
 
+// A mutated decode on the fused greedy path (mode != 0; the kernels' second argument, so the other kernels' argument
+// layout is untouched): the delta' rows in DecodeParams::noise hold only the parameters from off_log_w on (logit, i2h,
+// h2h: re-read at every step); the image projection and the embedding rows (read once, and only for the tokens taken)
+// form delta' = fp32(sigma z) / s (mode 1: SM-G-SUM / SM-VECTOR) or fp32(sigma z) * s (mode 2: SM-PROPORTIONAL)
+// themselves, from the sigma-scaled table slice at head_idx[member] and the mutation vector
+struct MutHead {
+    const float* head_noise;
+    const uint64_t* head_idx;
+    const float* mut_vec;
+    int32_t mode;
+};
+
 // launch kinds recorded next to the timing events
 #define DK_IMG 0
 #define DK_STEP 1        // fused step kernel (logits of t + cell of t + 1)
@@ -71,9 +83,10 @@ extern "C" hipError_t nicnes_decode_init();
 extern "C" hipError_t nicnes_decode_occupancy(int* coop_per_cu, int* sample_per_cu);
 // shifts the per-member and per-workgroup pointers of *p to member m0 (a decode of members m0.. on
 // its own stream; nslabs = the launch's row slabs)
-extern "C" void nicnes_decode_shift(DecodeParams* p, int m0, int nslabs);
-extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,
-                                           hipEvent_t* evs, int* kinds, int* n_launch);
+extern "C" void nicnes_decode_shift(DecodeParams* p, int m0, int nslabs, MutHead* mh);
+// mh: nullable (or mode 0): no decode-formed delta'
+extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, const MutHead* mh, int member_count, int nslabs,
+                                           hipStream_t stream, hipEvent_t* evs, int* kinds, int* n_launch);
 // zero seq_logprobs past the batch's last finishing step (rollouts = members x 2 of B rows; after a
 // no_exit decode of a batch spanning several slabs)
 extern "C" hipError_t nicnes_launch_lp_batch_exit(const int32_t* seq, float* lp, int rollouts, int B, int T,

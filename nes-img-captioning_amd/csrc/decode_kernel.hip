@@ -174,6 +174,54 @@ __device__ __forceinline__ void stage_store(float* buf, const TileDesc& d, int t
     }
 }
 
+// ---- a mutated member's delta' formed in the decode (MutHead, decode_kernel.h) -----------------------
+// fp32(sigma z) / s or fp32(sigma z) * s: the arithmetic of nicnes_mutate_kernel (update_kernels.hip, mutate1)
+__device__ __forceinline__ f32x4 mut_delta(const f32x4& z, const f32x4& v, int mode) {
+    f32x4 r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[e] = mode == 1 ? z[e] / v[e] : z[e] * v[e];
+    return r;
+}
+
+// the member's sigma-scaled table slice and the mutation vector over the parameters below off_log_w
+struct MutRes {
+    rsrc_t head_r, vec_r;
+    int mode;
+};
+__device__ __forceinline__ MutRes mut_res(const DecodeParams& p, const MutHead& mh, int member) {
+    MutRes m;
+    m.head_r = make_rsrc(mh.head_noise + mh.head_idx[member], 4u * (uint32_t)p.off_log_w);
+    m.vec_r = make_rsrc(mh.mut_vec, 4u * (uint32_t)p.off_log_w);
+    m.mode = mh.mode;
+    return m;
+}
+
+// stage_load / stage_store of a mutated member's image projection: z from the table slice, s from the vector,
+// delta' formed at the store (the loads' latency stays hidden behind the tile's MFMAs)
+struct StageRegsM {
+    StageRegs r;
+    f32x4 v[2];
+    float bv;
+};
+__device__ __forceinline__ void stage_load_m(rsrc_t theta_r, const MutRes& m, const TileDesc& d, int tid, StageRegsM& s) {
+    stage_load(theta_r, m.head_r, d, tid, s.r);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int f = tid + NTHREADS * u, row = f >> 5, q = f & 31;
+        const int rc = row < d.nvalid ? row : max(d.nvalid - 1, 0);
+        s.v[u] = ld4(m.vec_r, 4u * (d.w_off + (uint32_t)((d.row0 + rc) * d.ld + d.k0 + 4 * q)));
+    }
+    const int r = tid & 31;
+    s.bv = ld1(m.vec_r, 4u * (d.b_off + (uint32_t)(d.row0 + (r < d.nvalid ? r : 0))));
+}
+__device__ __forceinline__ void stage_store_m(float* buf, const TileDesc& d, int tid, const StageRegsM& s, int mode) {
+    StageRegs t = s.r;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) t.z[u] = mut_delta(s.r.z[u], s.v[u], mode);
+    t.bz = mode == 1 ? s.r.bz / s.bv : s.r.bz * s.bv;
+    stage_store(buf, d, tid, t);
+}
+
 // ---- MFMA tiles: acc += W_tile(32 x 128, LDS) . B(128 x 32, registers) -----------------------
 __device__ __forceinline__ f32x16 bias_init(const float* bias, int hh) {
     f32x16 acc;
@@ -1287,6 +1335,52 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_kernel(DecodeParam
     if (fused_path) PROF_MARK(81); else PROF_SPLIT(251);
 }
 
+// The same for a mutated member on the fused path (MutHead): delta' of img_embed formed at the stage store. The
+// 32-row kernel: its staging registers leave room for the vector's; the x it writes is nicnes_decode_img_kernel<4>'s.
+__global__ __launch_bounds__(NTHREADS) void nicnes_decode_img_mut_kernel(DecodeParams p, MutHead mh) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const SCtx<4> c = make_sctx<4>(p);
+    const MutRes mr = mut_res(p, mh, c.member);
+    PROF_MARK(80);
+    const float* fcm = p.fc + (p.member_batch ? (size_t)p.member_batch[c.member] * p.B_img * p.F : 0);
+    const rsrc_t fc_r = make_rsrc(fcm, 4u * (uint32_t)p.B_img * (uint32_t)p.F);
+    const int fr = c.row_valid ? (c.b + c.sgn * p.sign_off) / p.rpi : 0;      // the lane's fc row (its image)
+    const uint32_t lo = 4u * c.lane;
+    StageRegsM sr;
+    f32x16 accU[4];
+    const int nK = p.F >> 7;
+    const int ntile = nK * 4;
+    auto desc = [&](int n) {
+        TileDesc d;
+        d.w_off = (uint32_t)p.off_img_w; d.ld = p.F; d.row0 = 32 * (n % 4); d.nvalid = 32; d.k0 = 128 * (n / 4);
+        d.b_off = (uint32_t)p.off_img_b; d.pad_bias = 0.f;
+        return d;
+    };
+    stage_load_m(c.theta_r, mr, desc(0), c.tid, sr);
+    stage_store_m(lds, desc(0), c.tid, sr, mr.mode);
+    __syncthreads();
+    for (int kc = 0; kc < nK; ++kc) {
+        const uint32_t frow = 4u * (uint32_t)(fr * p.F + 128 * kc + 4 * c.hh);
+#pragma unroll
+        for (int U = 0; U < 4; ++U) {
+            const int n = kc * 4 + U;
+            if (n + 1 < ntile) stage_load_m(c.theta_r, mr, desc(n + 1), c.tid, sr);
+            const float* buf = lds + (n & 1) * STAGE_FLOATS;
+            if (kc == 0) accU[U] = bias_init(buf + 2 * SIGN_FLOATS + 32 * c.sgn, c.hh);
+            accU[U] = mfma_tile_fc(accU[U], buf + c.sgn * SIGN_FLOATS, fc_r, frow, c.lane);
+            if (n + 1 < ntile) stage_store_m(lds + ((n + 1) & 1) * STAGE_FLOATS, desc(n + 1), c.tid, sr, mr.mode);
+            __syncthreads();
+        }
+    }
+#pragma unroll
+    for (int U = 0; U < 4; ++U)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st1(c.scr_r, lo, X_SLOT(16 * U + r), accU[U][r]);
+    st1(c.scr_r, lo, U_SLOT, 1.0f);
+    if (c.tid == 0) p.alive[c.wg] = 1;
+    PROF_MARK(81);
+}
+
 // ========== t = 0 input on the fused path: 64-row stages, fc chunk as a register B operand ==========
 // x = img_embed(fc) of both signs for the workgroup's 128 rows (nets.py:194-195): 2 nK stages of 64 img_w rows
 // (unit blocks 0-1 for even stages, 2-3 for odd) x 128 k (chunk j >> 1), staged and double-buffered as the logit
@@ -1402,9 +1496,9 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_img64_kernel(DecodePar
 // logit tile, loaded during the previous step's last cell stage (PREFETCH: that load is issued)
 // SAMPLE: the sampled decode (nets.py:210-231): the logit loop stores its logits and stage sums (SampleStage), then
 // sample_pick draws each row's token with its uniform p.sample_u (fused path only)
-template <bool PAIRS, bool PREFETCH, bool SAMPLE = false>
+template <bool PAIRS, bool PREFETCH, bool SAMPLE = false, bool MUT = false>
 __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, float* lds, int t, Stage64Regs& s64,
-                                          bool& pre, float (&hB)[64], bool& hpre) {
+                                          bool& pre, float (&hB)[64], bool& hpre, const MutRes* mr = nullptr) {
     PROF_MARK(2 * (t + 1));
     const uint32_t lo = 4u * c.lane;
     const int nst = (p.V1 + 63) >> 6;
@@ -1569,8 +1663,12 @@ __device__ __forceinline__ bool step_body(const DecodeParams& p, const Ctx& c, f
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
                 const f32x4 w = ld4(c.theta_r, eo + 4u * (32 * T + 8 * a));
-                const f32x4 z = ld4(c.noise_r, eo + 4u * (32 * T + 8 * a));
-                const f32x4 delta = z;                      // fp32(sigma * z): the table is sigma-scaled
+                f32x4 delta;                                // fp32(sigma * z): the table is sigma-scaled
+                if constexpr (MUT)                          // a mutated member: the row's delta' formed here
+                    delta = mut_delta(ld4(mr->head_r, eo + 4u * (32 * T + 8 * a)),
+                                      ld4(mr->vec_r, eo + 4u * (32 * T + 8 * a)), mr->mode);
+                else
+                    delta = ld4(c.noise_r, eo + 4u * (32 * T + 8 * a));
                 const f32x4 x = c.sgn ? (w - delta) : (w + delta);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) xB[16 * T + 4 * a + e] = x[e];
@@ -1751,6 +1849,19 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_kernel(DecodePar
             __hip_atomic_store(p.slog_slots + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+
+// a mutated greedy decode on the fused path (MutHead: the embedding rows' delta' formed in step_body)
+template <bool PAIRS>
+__global__ __launch_bounds__(NTHREADS) void nicnes_decode_steps_mut_kernel(DecodeParams p, MutHead mh) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const Ctx c = make_ctx(p);
+    const MutRes mr = mut_res(p, mh, c.member);
+    Stage64Regs s64;
+    bool pre = false, hpre = false;
+    float hB[64];
+    for (int t = -1; t <= p.T; ++t)
+        if (!step_body<PAIRS, true, false, true>(p, c, lds, t, s64, pre, hB, hpre, &mr)) break;
 }
 
 // ========== split path: one member step over several workgroups =================================
@@ -2604,6 +2715,8 @@ extern "C" hipError_t nicnes_decode_init() {
         {(const void*)nicnes_decode_steps_kernel<true>, LDS64},
         {(const void*)nicnes_decode_steps_kernel<false>, LDS64},
         {(const void*)nicnes_decode_steps_kernel<false, true>, LDS64},
+        {(const void*)nicnes_decode_steps_mut_kernel<true>, LDS64},
+        {(const void*)nicnes_decode_steps_mut_kernel<false>, LDS64},
         {(const void*)nicnes_decode_logit_kernel<4, true>, LDS64},
         {(const void*)nicnes_decode_logit_kernel<4, false>, LDS64},
         {(const void*)nicnes_decode_logit_kernel<2, true>, LDS64},
@@ -2617,6 +2730,7 @@ extern "C" hipError_t nicnes_decode_init() {
         {(const void*)nicnes_decode_steps2_kernel<true>, LDS_CELL2},
         {(const void*)nicnes_decode_steps2_kernel<false>, LDS_CELL2},
         {(const void*)nicnes_decode_img_kernel<4>, LDS32},
+        {(const void*)nicnes_decode_img_mut_kernel, LDS32},
         {(const void*)nicnes_decode_img_kernel<2>, LDS32},
     };
     for (const auto& k : ks) {
@@ -2641,10 +2755,11 @@ extern "C" hipError_t nicnes_decode_occupancy(int* coop_per_cu, int* sample_per_
                                                         NTHREADS, LDS64);
 }
 
-extern "C" void nicnes_decode_shift(DecodeParams* p, int m0, int nslabs) {
+extern "C" void nicnes_decode_shift(DecodeParams* p, int m0, int nslabs, MutHead* mh) {
     const size_t wg0 = (size_t)m0 * (size_t)nslabs;        // workgroup index wg = member * slabs + slab
     const size_t rows = (size_t)m0 * 2 * (size_t)p->B * (size_t)p->T;
     p->noise_idx += m0;
+    if (mh && mh->head_idx) mh->head_idx += m0;
     if (p->member_batch) p->member_batch += m0;
     p->seq += rows;
     if (p->lp) p->lp += rows;
@@ -2655,13 +2770,17 @@ extern "C" void nicnes_decode_shift(DecodeParams* p, int m0, int nslabs) {
     if (p->coop_ctr) p->coop_ctr += wg0 * COOP_CTR_STRIDE;
 }
 
-extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_count, int nslabs, hipStream_t stream,
-                                           hipEvent_t* evs, int* kinds, int* n_launch) {
+extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, const MutHead* mh, int member_count, int nslabs,
+                                           hipStream_t stream, hipEvent_t* evs, int* kinds, int* n_launch) {
     const bool fused = p->G == 4 && p->S == 1;
     if (p->G != 4 && p->G != 2) return hipErrorInvalidValue;
     if (p->S < 1 || p->S > 64) return hipErrorInvalidValue;
     if (p->coop && (p->G != 4 || (p->S != 2 && p->S != 4) || !p->coop_ctr)) return hipErrorInvalidValue;
     if (p->sample_u && (!fused || p->coop)) return hipErrorInvalidValue;     // the sampled pick: fused path only
+    // delta' formed in the decode for the head parameters: the fused greedy kernels only
+    const bool mut = mh && mh->mode;
+    if (mut && (!fused || p->coop || p->sample_u || !mh->head_noise || !mh->head_idx || !mh->mut_vec))
+        return hipErrorInvalidValue;
     const int nl = fused || p->coop ? p->T + 3 : 3 + 2 * p->T;
     if (evs && nl + 1 > DECODE_MAX_EVENTS) return hipErrorInvalidValue;
     int ne = 0;
@@ -2699,7 +2818,10 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
         if (e != hipSuccess) return e;
         mark(DK_COOP);
     } else if (fused) {
-        hipLaunchKernelGGL(nicnes_decode_img64_kernel, dim3(member_count, nslabs), block, LDS64, stream, *p);
+        if (mut)
+            hipLaunchKernelGGL(nicnes_decode_img_mut_kernel, dim3(1, member_count, nslabs), block, LDS32, stream, *p, *mh);
+        else
+            hipLaunchKernelGGL(nicnes_decode_img64_kernel, dim3(member_count, nslabs), block, LDS64, stream, *p);
         mark(DK_IMG);
         const dim3 grid(member_count, nslabs);
         if (p->sample_u) {                                  // sampled decode: the exact lse, then the draw's pick
@@ -2707,7 +2829,11 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, int member_cou
             mark(DK_STEPS);
         } else {
 #if !DECODE_PROF
-            if (pairs)
+            if (mut && pairs)
+                hipLaunchKernelGGL(nicnes_decode_steps_mut_kernel<true>, grid, block, LDS64, stream, *p, *mh);
+            else if (mut)
+                hipLaunchKernelGGL(nicnes_decode_steps_mut_kernel<false>, grid, block, LDS64, stream, *p, *mh);
+            else if (pairs)
                 hipLaunchKernelGGL(nicnes_decode_steps_kernel<true>, grid, block, LDS64, stream, *p);
             else
                 hipLaunchKernelGGL(nicnes_decode_steps_kernel<false>, grid, block, LDS64, stream, *p);

@@ -100,6 +100,7 @@ struct nicnes_handle {
     float sc_sigma = 0.f;
     bool sc_valid = false;
     int mut_mode = 0;                 // nicnes_set_mutation: 0 plain, 1 divide, 2 multiply
+    bool mut_full = false;            // NICNES_MUT_FULL=1: materialise every parameter's delta' (no decode-formed head)
     float* mut_vec = nullptr;         // [D] sensitivity (mode 1) or |theta| scale (mode 2)
     float* dbuf = nullptr;            // [max_members, Dp] the members' mutated deltas (mode != 0)
     uint64_t* didx = nullptr;         // [max_members] k * Dp: row offsets of dbuf
@@ -368,6 +369,8 @@ int nicnes_create(const nicnes_config* cfg, int device, nicnes_handle** out) {
         h->force_exact = (fe && fe[0] == '1') ? 1 : 0;
         const char* lm = getenv("NICNES_LSE_MARGIN");
         if (lm && lm[0]) h->lse_margin = (float)atof(lm);
+        const char* mf = getenv("NICNES_MUT_FULL");
+        h->mut_full = mf && mf[0] == '1';
         const char* bl = getenv("NICNES_BOUNDED_LSE");
         if (bl && (bl[0] == '0' || bl[0] == '1')) h->bounded_mode = bl[0] - '0';
         const char* ds = getenv("NICNES_DECODE_STREAMS");
@@ -836,13 +839,8 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
         if (rc) return rc;
         HIPC(h, nicnes_launch_iota_stride(h->didx, h->cfg.max_members, (uint64_t)h->Dp, s));
     }
-    if (eval_theta) {
-    } else if (h->mut_mode) {      // safe / proportional mutations: the decode reads the members' delta' rows
-        HIPC(h, nicnes_launch_mutate(h->noise, h->nidx, count, h->D, sigma, h->mut_vec, h->mut_mode, h->dbuf, h->Dp, s));
-        p.noise = h->dbuf;
-        p.noise_idx = h->didx;
-    } else {                // the decode reads fp32(sigma * z) from the table scaled once per sigma
-        if (!h->noise_sc) {
+    if (!eval_theta) {      // fp32(sigma * z), the table scaled once per sigma: the plain decode's noise, and the
+        if (!h->noise_sc) { // sigma z a mutated fused decode forms the head parameters' delta' from (below)
             HIPC(h, hipDeviceSynchronize());
             int rc = dalloc(h, &h->noise_sc, (size_t)h->cfg.noise_len);
             if (rc) return rc;
@@ -852,8 +850,15 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
             h->sc_sigma = sigma;
             h->sc_valid = true;
         }
+    }
+    if (eval_theta) {
+    } else if (h->mut_mode) {      // safe / proportional mutations: the decode reads the members' delta' rows
+        p.noise = h->dbuf;         // (materialised below, once the decode path is known)
+        p.noise_idx = h->didx;
+    } else {
         p.noise = h->noise_sc;
     }
+    MutHead mh{nullptr, nullptr, nullptr, 0};
     p.fc = h->fc;
     p.member_batch = mb;
     p.seq = seq_out ? seq_out : h->seq;
@@ -936,6 +941,16 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     p.part = h->part;
     p.coop = !sampled && coop_fits(h, G, nslabs, S, count) ? 1 : 0;
     p.coop_launch = h->coop_launch;
+    if (!eval_theta && h->mut_mode) {
+        // the members' delta' rows. On the fused greedy path only the parameters from off_log_w on (logit, i2h, h2h,
+        // which every step re-reads) are materialised; the decode forms the image projection's and the embedding
+        // rows' delta' itself from sigma z and the vector (DecodeParams::mut_head): 5.6 of the 11.5 MB per member
+        const bool head = !sampled && !p.coop && G == 4 && S == 1 && !h->mut_full;
+        const int64_t j0 = head ? h->off[3] : 0;
+        HIPC(h, nicnes_launch_mutate(h->noise + j0, h->nidx, count, h->D - j0, sigma, h->mut_vec + j0, h->mut_mode,
+                                     h->dbuf + j0, h->Dp, s));
+        if (head) mh = MutHead{h->noise_sc, h->nidx, h->mut_vec, h->mut_mode};
+    }
     p.test_stall_ms = h->test_stall_left != 0 ? h->test_stall_ms : 0;
     if (p.coop && h->test_stall_ms && h->test_stall_left > 0) --h->test_stall_left;
     // log-probs of a batch spread over several slabs: every slab runs to T, then the steps after the
@@ -984,17 +999,18 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
         for (int i = 0; i < nstr; ++i) {
             const int a = (int)((int64_t)count * i / nstr), b = (int)((int64_t)count * (i + 1) / nstr);
             DecodeParams pi = p;
-            nicnes_decode_shift(&pi, a, nslabs);
+            MutHead mi = mh;
+            nicnes_decode_shift(&pi, a, nslabs, &mi);
             hipStream_t si = i == 0 ? s : h->sx[i - 1];
             if (i > 0) HIPC(h, hipStreamWaitEvent(si, h->ev_fork, 0));
-            HIPC(h, nicnes_launch_decode(&pi, b - a, nslabs, si, nullptr, nullptr, nullptr));
+            HIPC(h, nicnes_launch_decode(&pi, &mi, b - a, nslabs, si, nullptr, nullptr, nullptr));
         }
         for (int i = 0; i < nstr - 1; ++i) {
             HIPC(h, hipEventRecord(h->ev_join[i], h->sx[i]));
             HIPC(h, hipStreamWaitEvent(s, h->ev_join[i], 0));
         }
     } else {
-        HIPC(h, nicnes_launch_decode(&p, count, nslabs, s, h->timing ? h->dev : nullptr, h->dev_kind, &n_ev));
+        HIPC(h, nicnes_launch_decode(&p, &mh, count, nslabs, s, h->timing ? h->dev : nullptr, h->dev_kind, &n_ev));
     }
     h->n_dev = h->timing ? n_ev : 0;
     h->multi_stream = nstr > 1;
