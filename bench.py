@@ -577,6 +577,10 @@ def main():
             kname = 'nicnes_decode_steps2_kernel'
         else:
             kname = 'nicnes_decode_steps_kernel' if ph['step_launches'] == 1 else 'nicnes_decode_step_kernel'
+            if args.mutation and G == 4 and ph['step_launches'] == 1:
+                # a mutated member's embedding rows' delta' formed in the decode: its own kernel (no committed PMC
+                # profile: the line reports traffic null rather than the plain kernel's counters)
+                kname = 'nicnes_decode_steps_mut_kernel'
         n_step = ph['step_launches']
         step_ms = float(np.mean([q['step_ms'] for q in phases])) / n_step
         step_flop = step_flops_per_member(B) * P_local / n_step
