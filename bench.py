@@ -148,6 +148,9 @@ def load_pmc(kernel, P, B, pairs=True):
     if key is None:
         return None, None
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_%s_p%d_b%d.json' % (key, P, B))), reverse=True)
+    if key == 'steps' and not pairs:     # the exact-lse instantiation's profile (measured on the trained-like theta)
+        files += sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_steps-trained_p%d_b%d.json' % (P, B))),
+                        reverse=True)
     if not files:
         return None, None
     symbol = PMC_SYMBOLS.get((key, pairs if key != 'sampled' else False))
@@ -593,9 +596,9 @@ def main():
     achieved = step_flop / (step_ms / 1e3) / 1e12
     # counter figures of the same kernel and workload from the committed rocprofv3 PMC profile
     # (a profile-derived constant: PMC passes cannot run inside the timed bench process)
-    # (the greedy-only bounded-lse instantiation unless log-probs are written or NICNES_BOUNDED_LSE=0; the engine's
-    # adaptive policy may run some decodes of a peaked theta on the exact one)
-    pairs_run = args.fitness == 'greedy' and os.environ.get('NICNES_BOUNDED_LSE', '2') != '0'
+    # (the instantiation the last timed decode ran: the greedy-only bounded-lse one, or the exact one -- log-probs
+    # written, NICNES_BOUNDED_LSE=0, or the engine's adaptive policy on a peaked theta)
+    pairs_run = args.fitness == 'greedy' and eng.last_decode_bounded()
     pmc, pmc_stale = load_pmc(kname, P_local, B, pairs_run)
     traffic = pmc['derived'].get('hbm_bytes_per_launch') if pmc else None
     hbm_peak_bytes = HBM_PEAK_GBS * 1e9 * step_ms / 1e3

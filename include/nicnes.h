@@ -324,6 +324,11 @@ int nicnes_sum_sensitivity(nicnes_handle* h, int32_t rows, float underflow, floa
 /* the decode path an evaluate of `count` members of a B-image batch would take: 0 fused (one launch,
  * one workgroup per member slab), 1 split (two launches per step), 2 coop (the split shape in one launch) */
 int nicnes_decode_path(nicnes_handle* h, int32_t B, int32_t count, int32_t* out_host);
+/* the log-sum-exp mode of the last greedy decode enqueued: 1 the pair-bounded lse (greedy-only decodes while the
+ * engine's adaptive policy allows it), 0 the exact exp-sum (log-probs written, NICNES_BOUNDED_LSE=0, or the policy's
+ * exact stretch after a bounded decode needed exact passes). Measurement bookkeeping for bench.py (which kernel
+ * instantiation a line's PMC counters belong to); no reference counterpart. */
+int nicnes_last_decode_lse(nicnes_handle* h, int32_t* bounded_host);
 
 #ifdef __cplusplus
 }

@@ -149,6 +149,7 @@ struct nicnes_handle {
     int bounded_mode = 2;     // NICNES_BOUNDED_LSE: 0 never, 1 always, 2 adaptive
     int exact_left = 0;
     int last_bounded = 0;
+    int last_decode_bounded = 0;      // nicnes_last_decode_lse: the lse mode of the last decode enqueued
     int32_t fb_seen = 0;
     int32_t* stats_host = nullptr;
     hipEvent_t stats_ev = nullptr;
@@ -887,6 +888,7 @@ static int evaluate_impl(nicnes_handle* h, uint64_t iteration, int32_t member_be
     bool bounded = h->bounded_mode == 1 || (h->bounded_mode == 2 && h->exact_left == 0);
     if (h->bounded_mode == 2 && h->exact_left > 0 && !p.lp) --h->exact_left;
     p.bounded_lse = bounded ? 1 : 0;
+    h->last_decode_bounded = (bounded && !p.lp) ? 1 : 0;
     // rows per sign: all of the rollout's rows, or the first half (eval_theta; sign - takes rows half + b)
     const int rows = eval_theta ? (rows_total + 1) / 2 : rows_total;
     int G = 0, nslabs = 0, S = 0;
@@ -1360,6 +1362,12 @@ int nicnes_set_decode_streams(nicnes_handle* h, int32_t n) {
 int nicnes_set_decode_coop(nicnes_handle* h, int32_t mode) {
     if (!h || (mode != 0 && mode != 1)) return NICNES_ERR_INVALID;
     h->coop_mode = mode;
+    return NICNES_OK;
+}
+
+int nicnes_last_decode_lse(nicnes_handle* h, int32_t* bounded_host) {
+    if (!h || !bounded_host) return NICNES_ERR_INVALID;
+    *bounded_host = h->last_decode_bounded;
     return NICNES_OK;
 }
 

@@ -22,7 +22,8 @@ EXPORTS = ['nicnes_param_count', 'nicnes_param_offsets', 'nicnes_create', 'nicne
            'nicnes_noise_vectors', 'nicnes_set_batches', 'nicnes_evaluate_batches', 'nicnes_set_mutation',
            'nicnes_set_mutation_proportional', 'nicnes_theta_zeros',
            'nicnes_set_decode_coop', 'nicnes_decode_path', 'nicnes_sum_sensitivity', 'nicnes_grad_partial_range',
-           'nicnes_evaluate_theta', 'nicnes_set_sample_draws', 'nicnes_set_rows_per_image']
+           'nicnes_evaluate_theta', 'nicnes_set_sample_draws', 'nicnes_set_rows_per_image',
+           'nicnes_last_decode_lse']
 
 
 class NicnesConfig(ctypes.Structure):
@@ -96,6 +97,7 @@ def lib(path=None):
         'nicnes_set_decode_streams': (c.c_int, [vp, i32]),
         'nicnes_set_decode_coop': (c.c_int, [vp, i32]),
         'nicnes_decode_path': (c.c_int, [vp, i32, i32, vp]),
+        'nicnes_last_decode_lse': (c.c_int, [vp, vp]),
         'nicnes_sum_sensitivity': (c.c_int, [vp, i32, f32, vp, vp]),
         'nicnes_comm_unique_id': (c.c_int, [vp]),
         'nicnes_comm_init': (c.c_int, [vp, i32, i32, vp]),

@@ -396,6 +396,12 @@ class Engine:
         check(self.L.nicnes_set_decode_coop(self.h, int(mode)), self.h, 'set_decode_coop')
         self.coop_mode = int(mode)
 
+    def last_decode_bounded(self):
+        """True when the last greedy decode enqueued used the pair-bounded lse (the steps kernel's PAIRS instantiation)."""
+        out = ctypes.c_int32()
+        check(self.L.nicnes_last_decode_lse(self.h, ctypes.byref(out)), self.h, 'last_decode_lse')
+        return bool(out.value)
+
     def decode_path(self, B=None, count=1):
         """'fused', 'split' or 'coop': the decode path an evaluate of `count` members would take."""
         out = ctypes.c_int32()
