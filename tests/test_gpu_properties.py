@@ -194,3 +194,22 @@ def test_logprobs_after_a_slab_exit_match_oracle(eng, S, G, coop):
     assert np.array_equal(seq[ok], oseq[ok])
     assert np.abs(lp[ok] - olp[ok]).max() <= 1e-5
     assert (lp[:, fin.max() + 1:] == 0).all() and (olp[:, fin.max() + 1:] == 0).all()
+
+
+def test_last_decode_lse_mode_reports_the_instantiation(eng):
+    """nicnes_last_decode_lse (bench.py's PMC attribution): a greedy-only decode at xavier theta runs the pair-bounded
+    lse, one with log-probs written the exact exp-sum; the tokens agree. (A fresh handle: the module engine's adaptive
+    policy may be in an exact stretch after the forced-tie tests.)"""
+    import nicnes
+    e = nicnes.Engine(max_batch=32, max_members=2, noise_len=NOISE_LEN, noise_seed=11)
+    try:
+        e.set_noise_table(eng._table_np)
+        dims = O.Dims()
+        _load(e, O.make_theta(dims, 0, 1.0, 0.0), _fc(32))
+        _, s_b = e.evaluate(5, 0, 2, SIGMA, return_seq=True)
+        assert e.last_decode_bounded()
+        _, s_e, _ = e.evaluate(5, 0, 2, SIGMA, return_seq=True, return_lp=True)
+        assert not e.last_decode_bounded()
+        assert torch.equal(s_b, s_e)
+    finally:
+        e.close()
