@@ -2495,251 +2495,6 @@ __global__ __launch_bounds__(NTHREADS) void nicnes_decode_coop_kernel(DecodePara
         if (!coop_step<PAIRS, S>(p, c, q, lds, t, s64, pre, hB, ctr, phase)) break;
 }
 
-// ========== coop path of 64-row slabs (G = 2): the split shape of B <= 64 in ONE launch =================
-// mscoco_nes.json's own batch_size 64 at 64 members per GPU (the metric's population over 8 GPUs): S workgroups per
-// member slab split the vocabulary as the G = 2 split path does (nicnes_decode_logit_kernel<2> +
-// nicnes_decode_cell_kernel<2>), in one persistent launch with the G = 4 coop kernel's two hand-offs per step. Wave
-// w = sign (w >> 2) x 32-row group ((w >> 1) & 1) x tile half (w & 1): the two halves of a row group scan opposite
-// 32-row halves of every 64-row stage of the workgroup's range (nh = 2 partial states per row and range, merged in
-// the split path's order, so coop and split give identical bits); in the cell, half 0 runs the i2h chain over x and
-// half 1 the h2h chain over h, handed over in LDS, and half 0 folds. h' crosses steps in the row group's scratch
-// (parity slots) and is read back by both halves. Hand-offs, counters, spin bounds and residency as in coop_step.
-template <bool PAIRS, int S>
-__device__ __forceinline__ bool coop_step2(const DecodeParams& p, const SCtx<2>& c, int q, float* lds, int t,
-                                           Stage64Regs& s64, bool& pre, float (&hB)[64], uint32_t* ctr, uint32_t& phase) {
-    const uint32_t lo = 4u * c.lane;
-    const int nst = (p.V1 + 63) >> 6;
-    const int s0 = q * nst / S, s1 = (q + 1) * nst / S;
-    __builtin_assume(s1 > s0);                     // (coop_fits: nst >= S; as in coop_step)
-    const int nb = 4 / S, m0 = 5 * nb * q, m1 = m0 + 5 * nb;
-    const bool nl = t > 0;
-    const bool folder = c.hf == 0;                 // waves that own the rows' token and the cell fold
-    const uint64_t nidx = p.noise_idx[c.member];
-    const float unf_prev = (nl && folder) ? ld1(c.scr_r, lo, U_SLOT) : 0.f;
-    if (t < 0) {
-#pragma unroll
-        for (int i = 0; i < 64; ++i) hB[i] = 0.f;               // h = 0 before the first cell
-    }
-#pragma unroll
-    for (int i = 0; i < 64; ++i) pin(hB[i]);
-    const uint32_t ib = (uint32_t)p.off_i2h_b, hb = (uint32_t)p.off_h2h_b, bmin = min(ib, hb);
-    auto csrc = [&](int m) {                                     // gate tile m: i2h rows | h2h rows
-        const uint32_t r = gate_row(m);
-        StageSrc Sx;
-        Sx.w_r = c.theta_r; Sx.z_r = c.noise_r; Sx.b_r = c.theta_r; Sx.bz_r = c.noise_r;
-        Sx.so_a = 4u * ((uint32_t)p.off_i2h_w + 128u * r);
-        Sx.so_b = 4u * ((uint32_t)p.off_h2h_w + 128u * r);
-        Sx.bso = 4u * (bmin + r);
-        Sx.bda = 4u * (ib - bmin); Sx.bdb = 4u * (hb - bmin);
-        Sx.valid = 64;
-        return Sx;
-    };
-    int it = 0;                                   // token fed to the next cell (0 = BOS at t = 0)
-    bool cell_pre = false;                        // s64 holds the cell's first gate tile
-    if (nl) {
-        RowState st;
-        row_state_init(st);
-        auto tail = [&]() __attribute__((always_inline)) {
-            if (t < p.T) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
-        };
-        logit_stages<2, PAIRS, false>(lds, p, nidx, c.wave, c.sgn, c.hf, hB, s0, s1, st, s64, pre, tail);
-        cell_pre = t < p.T;
-        {   // phase A: this range's partial state of the wave's rows and tile half, write-through
-            const rsrc_t part_r = make_rsrc(part_ptr(p, c.wg, q, 0), PART_FLOATS * 4);
-            const uint32_t po = 4u * (uint32_t)(c.wave * (7 * 64) + lane_fresh());
-            st1_wt(part_r, po, 0u, st.m);
-            st1_wt(part_r, po, 256u, st.s);
-            st1_wt(part_r, po, 512u, st.r0v);
-            st1_wt(part_r, po, 768u, __builtin_bit_cast(float, st.r0i));
-            st1_wt(part_r, po, 1024u, st.r1v);
-            st1_wt(part_r, po, 1280u, __builtin_bit_cast(float, st.r1i));
-            st1_wt(part_r, po, 1536u, st.ev);
-        }
-        coop_arrive(ctr);
-        ++phase;
-#if !(DECODE_ABLATE & 128)
-        if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
-#endif
-        float m = 0.f, lse = 0.f;
-        int tok = 0x7fffffff;
-        bool ovf = false;
-        if (folder) {                              // the 2 S partials of the rows: k = range * 2 + half
-            Part8 pr;
-            load_part8(p, c.wg, c.wave, lane_fresh(), 2, 2 * S, 0, pr);
-            merge_partials(p, c.wg, c.wave, lane_fresh(), 2, 2 * S, pr, PAIRS, m, lse, tok, ovf);
-        }
-        if (__syncthreads_or((p.force_exact || ovf) ? 1 : 0)) {
-            merge_exact(p, lds, c.wg, c.theta_r, c.noise_r, c.tid, c.sgn, c.hh, c.wave, c.lane, 2, 2 * S, hB, folder,
-                        PAIRS, m, lse, tok);
-            if (q == 0 && c.tid == 0) atomicAdd(p.stats + 0, 1);
-            cell_pre = false;                      // the exact sweep staged through LDS with its own registers
-        }
-        if (tok >= p.V1) tok = 0;                 // every logit NaN: end the caption (fused kernel rule)
-        const bool unfinished = unf_prev != 0.f && tok > 0;
-        it = (unfinished || p.no_mask) ? tok : 0;
-        if (folder) {
-            st1(c.scr_r, lo, U_SLOT, unfinished ? 1.f : 0.f);
-#if !DECODE_PROF
-            if (q == 0 && c.hh == 0 && c.row_valid) {
-                const size_t o = (((size_t)c.member * 2 + c.sgn) * p.B + c.b) * p.T + (t - 1);
-                p.seq[o] = it;
-                if (p.lp) p.lp[o] = -lse;         // seq_logprobs[:, t-1] (nets.py:208,241)
-            }
-#endif
-        }
-        // every workgroup of the group reaches the same decision (the reference stops here, nets.py:242-243)
-        if (!__syncthreads_or(((folder && unfinished && c.row_valid) || p.no_exit) ? 1 : 0)) return false;
-    }
-    if (t >= p.T) return false;
-
-    // ---- LSTM cell of step t+1, gate tiles of this workgroup's unit blocks: half 0 i2h over x, half 1 h2h over h
-    float xB[64];
-    if (!folder) {
-#pragma unroll
-        for (int i = 0; i < 64; ++i) xB[i] = 0.f;
-    } else if (t < 0) {                                          // x = img_embed(fc) (nets.py:194-195)
-#pragma unroll
-        for (int i = 0; i < 64; ++i) xB[i] = ld1(c.scr_r, lo, X_SLOT(i));
-    } else {                                                     // x = embed(it) (nets.py:196-199)
-        const uint32_t eo = 4u * ((uint32_t)p.off_emb_w + (uint32_t)it * 128u + 4u * c.hh);
-#pragma unroll
-        for (int T = 0; T < 4; ++T)
-#pragma unroll
-            for (int a = 0; a < 4; ++a) {
-                const f32x4 w = ld4(c.theta_r, eo + 4u * (32 * T + 8 * a));
-                const f32x4 z = ld4(c.noise_r, eo + 4u * (32 * T + 8 * a));
-                const f32x4 x = c.sgn ? (w - z) : (w + z);         // the table is sigma-scaled
-#pragma unroll
-                for (int e = 0; e < 4; ++e) xB[16 * T + 4 * a + e] = x[e];
-            }
-    }
-#pragma unroll
-    for (int i = 0; i < 64; ++i) pin(xB[i]);
-    const int hpar = (t + 1) & 1;
-    if (!cell_pre) stage64_load(csrc(m0), c.wave * 64 + lane_fresh(), s64);
-    stage64_store(lds, 64, c.wave * 64 + lane_fresh(), s64);
-    __syncthreads();
-    f32x16 hold;
-    auto fold = [&](int m, const f32x16& s_, const f32x16& cpre) __attribute__((always_inline)) {
-        const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
-        const int U = m / 5, j5 = m % 5;
-        if (j5 == 0) {                                           // g1
-            hold = s_;
-        } else if (j5 == 1) {                                    // g = max(g1, g2)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) hold[r] = hold[r] > s_[r] ? hold[r] : s_[r];
-        } else if (j5 == 2) {                                    // ig * g
-#pragma unroll
-            for (int r = 0; r < 16; ++r) hold[r] = CELL_SIG(s_[r]) * hold[r];
-        } else if (j5 == 3) {                                    // c' = f * c + ig * g
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float fcv = CELL_SIG(s_[r]) * cpre[r];
-                const float cn = fcv + hold[r];
-                st1(c.scr_r, lo_, C_SLOT(16 * U + r), cn);      // c: read back only by this workgroup
-                hold[r] = cn;
-            }
-        } else {                                                 // h' = o * tanh(c'), handed to the group
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                st1_wt(c.scr_r, lo_, HP_SLOT(hpar, 16 * U + r), CELL_SIG(s_[r]) * CELL_TANH(hold[r]));
-        }
-    };
-    auto load_c = [&](int m) __attribute__((always_inline)) {   // c of the f tile's unit block
-        f32x16 cp;
-        const uint32_t lo_ = 4u * (uint32_t)lane_fresh();
-#pragma unroll
-        for (int r = 0; r < 16; ++r) cp[r] = (m % 5 == 3 && t >= 0 && folder) ? ld1(c.scr_r, lo_, C_SLOT(16 * (m / 5) + r)) : 0.f;
-        return cp;
-    };
-    float* xch = lds + 2 * STAGE64_FLOATS + (c.sgn * 2 + c.grp) * 1024;   // h2h half -> i2h half
-    const bool lpf = t >= 0;                                              // the next step's first logit tile
-#pragma unroll 1
-    for (int m = m0; m < m1; ++m) {
-        const f32x16 cpre = load_c(m);
-        __builtin_amdgcn_sched_barrier(0);
-        if (m + 1 < m1) {
-            stage64_load(csrc(m + 1), c.wave * 64 + lane_fresh(), s64);
-        } else if (lpf) {
-            const LaneOffs lo_ = lane_offs(c.wave, 128u);
-            stage64_load_o(logit_src(p, nidx, s0), lo_, c.wave < 2, s64);
-        }
-        const float* buf = lds + ((m - m0) & 1) * STAGE64_FLOATS;
-        const float* w1 = buf + c.sgn * (64 * LDS_ROW) + 32 * c.hf * LDS_ROW;
-        const float* b1 = buf + 2 * 64 * LDS_ROW + 64 * c.sgn + 32 * c.hf;
-        f32x16 a = bias_init(b1, lane_fresh() >> 5);
-        if (folder) a = mfma_tile(a, w1, xB, lane_fresh());
-        else if (t >= 0) a = mfma_tile(a, w1, hB, lane_fresh());   // h = 0 before the first cell: the bias
-        if (!folder) {
-            const int l = lane_fresh();
-#pragma unroll
-            for (int r = 0; r < 16; ++r) xch[r * 64 + l] = a[r];
-        }
-        __syncthreads();
-        if (folder) {
-            const int l = lane_fresh();
-            f32x16 a1;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) a1[r] = xch[r * 64 + l];
-            fold(m, a + a1, cpre);                               // i2h(x) + h2h(h), nets.py:109-111
-        }
-        if (m + 1 < m1) stage64_store(lds + ((m - m0 + 1) & 1) * STAGE64_FLOATS, 64, c.wave * 64 + lane_fresh(), s64);
-        __syncthreads();
-    }
-    pre = lpf;
-    // ---- phase B: h_{t+1} complete in the group -> both halves of every row group read all of it
-    coop_arrive(ctr);
-    ++phase;
-#if !(DECODE_ABLATE & 128)
-    if (!coop_wait(ctr, (uint32_t)S * phase, p.stats)) return false;
-#endif
-#pragma unroll
-    for (int i = 0; i < 64; ++i) hB[i] = ld1(c.scr_r, lo, HP_SLOT(hpar, i));
-    return true;
-}
-
-// grid: S x member slabs workgroups (64-row slabs), L = blockIdx.x -> range q = L % S of group L / S
-template <bool PAIRS, int S>
-__global__ __launch_bounds__(NTHREADS) void nicnes_decode_coop2_kernel(DecodeParams p, int nslabs) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int L = blockIdx.x, q = L % S, gi = L / S;
-    SCtx<2> c;
-    c.tid = threadIdx.x;
-    c.lane = c.tid & 63;
-    c.wave = __builtin_amdgcn_readfirstlane(c.tid >> 6);
-    c.sgn = c.wave >> 2;
-    c.grp = (c.wave >> 1) & 1;
-    c.hf = c.wave & 1;
-    c.hh = c.lane >> 5;
-    c.q = q;
-    c.member = gi / nslabs;
-    c.slab = gi % nslabs;
-    c.wg = gi;
-    c.b = c.slab * 64 + c.grp * 32 + (c.lane & 31);
-    c.row_valid = row_ok(p, c.b, c.sgn);
-    c.bc = c.row_valid ? c.b : 0;
-    const uint64_t nidx = p.noise_idx[c.member];
-    const uint32_t Dbytes = 4u * (uint32_t)p.D;
-    c.theta_r = make_rsrc(p.theta, Dbytes);
-    c.noise_r = make_rsrc(p.noise + nidx, Dbytes);
-    float* wscr = p.scratch + ((size_t)c.wg * 4 + c.sgn * 2 + c.grp) * (SCR_SLOTS * 64);   // make_sctx<2>'s slots
-    c.scr_r = make_rsrc(wscr, SCR_SLOTS * 64 * 4);
-    uint32_t* ctr = p.coop_ctr + (size_t)gi * COOP_CTR_STRIDE;
-    uint32_t phase = 0;
-    if (p.test_stall_ms && L == 0) {               // test hook: a partner that arrives past the spin bound
-        if (c.tid == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__builtin_amdgcn_s_memrealtime() - t0 < 100000ull * p.test_stall_ms) __builtin_amdgcn_s_sleep(127);
-        }
-        __syncthreads();
-    }
-    Stage64Regs s64;
-    bool pre = false;
-    float hB[64];
-    for (int t = -1; t <= p.T; ++t)
-        if (!coop_step2<PAIRS, S>(p, c, q, lds, t, s64, pre, hB, ctr, phase)) break;
-}
-
 // ========== fused path for 64-row slabs (G = 2): every step of a workgroup in one launch =========
 // B <= 64 (mscoco_nes.json's own batch_size 64) with one workgroup per member slab (S = 1): wave w =
 // sign (w >> 2) x 32-row group ((w >> 1) & 1) x tile half (w & 1), as on the split path. Per step the
@@ -2972,10 +2727,6 @@ extern "C" hipError_t nicnes_decode_init() {
         {(const void*)nicnes_decode_coop_kernel<true, 4>, LDS64},
         {(const void*)nicnes_decode_coop_kernel<false, 4>, LDS64},
         {(const void*)nicnes_decode_cell_kernel<2>, LDS_CELL2},
-        {(const void*)nicnes_decode_coop2_kernel<true, 2>, LDS_CELL2},
-        {(const void*)nicnes_decode_coop2_kernel<false, 2>, LDS_CELL2},
-        {(const void*)nicnes_decode_coop2_kernel<true, 4>, LDS_CELL2},
-        {(const void*)nicnes_decode_coop2_kernel<false, 4>, LDS_CELL2},
         {(const void*)nicnes_decode_steps2_kernel<true>, LDS_CELL2},
         {(const void*)nicnes_decode_steps2_kernel<false>, LDS_CELL2},
         {(const void*)nicnes_decode_img_kernel<4>, LDS32},
@@ -2990,17 +2741,12 @@ extern "C" hipError_t nicnes_decode_init() {
 }
 
 extern "C" hipError_t nicnes_decode_occupancy(int* coop_per_cu, int* sample_per_cu) {
-    const struct { const void* f; size_t b; } coop[] = {
-        {(const void*)nicnes_decode_coop_kernel<true, 2>, LDS64}, {(const void*)nicnes_decode_coop_kernel<false, 2>, LDS64},
-        {(const void*)nicnes_decode_coop_kernel<true, 4>, LDS64}, {(const void*)nicnes_decode_coop_kernel<false, 4>, LDS64},
-        {(const void*)nicnes_decode_coop2_kernel<true, 2>, LDS_CELL2},
-        {(const void*)nicnes_decode_coop2_kernel<false, 2>, LDS_CELL2},
-        {(const void*)nicnes_decode_coop2_kernel<true, 4>, LDS_CELL2},
-        {(const void*)nicnes_decode_coop2_kernel<false, 4>, LDS_CELL2}};
+    const void* coop[] = {(const void*)nicnes_decode_coop_kernel<true, 2>, (const void*)nicnes_decode_coop_kernel<false, 2>,
+                          (const void*)nicnes_decode_coop_kernel<true, 4>, (const void*)nicnes_decode_coop_kernel<false, 4>};
     int lo = 1 << 30;
-    for (const auto& k : coop) {
+    for (const void* f : coop) {
         int n = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k.f, NTHREADS, k.b);
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, NTHREADS, LDS64);
         if (e != hipSuccess) return e;
         lo = n < lo ? n : lo;
     }
@@ -3029,7 +2775,7 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, const MutHead*
     const bool fused = p->G == 4 && p->S == 1;
     if (p->G != 4 && p->G != 2) return hipErrorInvalidValue;
     if (p->S < 1 || p->S > 64) return hipErrorInvalidValue;
-    if (p->coop && ((p->S != 2 && p->S != 4) || !p->coop_ctr)) return hipErrorInvalidValue;
+    if (p->coop && (p->G != 4 || (p->S != 2 && p->S != 4) || !p->coop_ctr)) return hipErrorInvalidValue;
     if (p->sample_u && (!fused || p->coop)) return hipErrorInvalidValue;     // the sampled pick: fused path only
     // delta' formed in the decode for the head parameters: the fused greedy kernels only
     const bool mut = mh && mh->mode;
@@ -3054,29 +2800,21 @@ extern "C" hipError_t nicnes_launch_decode(const DecodeParams* p, const MutHead*
         hipError_t e = hipMemsetAsync(p->coop_ctr, 0, (size_t)member_count * nslabs * COOP_CTR_STRIDE * sizeof(uint32_t),
                                       stream);
         if (e != hipSuccess) return e;
-        if (p->G == 4)
-            hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(p->S, member_count, nslabs), block, LDS32, stream, *p);
-        else
-            hipLaunchKernelGGL(nicnes_decode_img_kernel<2>, dim3(p->S, member_count, nslabs), block, LDS32, stream, *p);
+        hipLaunchKernelGGL(nicnes_decode_img_kernel<4>, dim3(p->S, member_count, nslabs), block, LDS32, stream, *p);
         mark(DK_IMG);
         const dim3 grid(p->S * member_count * nslabs);
-        const void* kf = p->G == 4 ? (p->S == 2 ? (pairs ? (const void*)nicnes_decode_coop_kernel<true, 2>
-                                                         : (const void*)nicnes_decode_coop_kernel<false, 2>)
-                                                : (pairs ? (const void*)nicnes_decode_coop_kernel<true, 4>
-                                                         : (const void*)nicnes_decode_coop_kernel<false, 4>))
-                                   : (p->S == 2 ? (pairs ? (const void*)nicnes_decode_coop2_kernel<true, 2>
-                                                         : (const void*)nicnes_decode_coop2_kernel<false, 2>)
-                                                : (pairs ? (const void*)nicnes_decode_coop2_kernel<true, 4>
-                                                         : (const void*)nicnes_decode_coop2_kernel<false, 4>));
-        const size_t lds_b = p->G == 4 ? LDS64 : LDS_CELL2;
+        const void* kf = p->S == 2 ? (pairs ? (const void*)nicnes_decode_coop_kernel<true, 2>
+                                            : (const void*)nicnes_decode_coop_kernel<false, 2>)
+                                   : (pairs ? (const void*)nicnes_decode_coop_kernel<true, 4>
+                                            : (const void*)nicnes_decode_coop_kernel<false, 4>);
         DecodeParams pk = *p;
         int ns = nslabs;
         void* args[] = {&pk, &ns};
         // the group hand-offs need every workgroup resident at once: the engine bounds the grid by the occupancy query
         // (coop_fits); the cooperative launch (opt-in) has the runtime check it too and fail instead of queueing a
         // workgroup behind its partners
-        e = p->coop_launch ? hipLaunchCooperativeKernel(kf, grid, block, args, lds_b, stream)
-                           : hipLaunchKernel(kf, grid, block, args, lds_b, stream);
+        e = p->coop_launch ? hipLaunchCooperativeKernel(kf, grid, block, args, LDS64, stream)
+                           : hipLaunchKernel(kf, grid, block, args, LDS64, stream);
         if (e != hipSuccess) return e;
         mark(DK_COOP);
     } else if (fused) {

@@ -252,7 +252,7 @@ void decode_shape(const nicnes_handle* h, int B, int count, int* G, int* nslabs,
 // 4 logit ranges per member slab, and every workgroup of the launch resident at once (one per CU).
 bool coop_fits(const nicnes_handle* h, int G, int nslabs, int S, int count) {
     // (nst >= S: coop_step assumes every logit range non-empty; the split path handles empty ranges)
-    return h->coop_mode && (G == 4 || G == 2) && (S == 2 || S == 4) && (h->V1 + 63) / 64 >= S &&
+    return h->coop_mode && G == 4 && (S == 2 || S == 4) && (h->V1 + 63) / 64 >= S &&
            (int64_t)count * nslabs * S <= (int64_t)h->coop_occ * h->n_cu;
 }
 

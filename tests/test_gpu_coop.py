@@ -1,8 +1,7 @@
 """GPU parity of the coop decode path (nicnes_decode_coop_kernel): the split shape (128-row slabs,
 S = 2 or 4 logit ranges per member slab) in ONE persistent launch whose workgroups hand the partial
 greedy states and h' to each other inside it. This is the shape of 64 and 128 members per GPU at
-B = 128: configs[1], and the metric's pop=512 over 8 and 4 GPUs. Since round 6 also 64-row slabs
-(nicnes_decode_coop2_kernel, G = 2): mscoco_nes.json's batch_size 64 at 64 / 128 members per GPU.
+B = 128: configs[1], and the metric's pop=512 over 8 and 4 GPUs.
 
 Bars: tokens and log-probs bit-identical to the two-launch split path (same merge order of the
 partials), tokens equal to the C oracle except after a step it marks lse-fragile, CIDEr-D fitness to
@@ -73,9 +72,8 @@ def test_decode_path_rule(eng):
     assert eng.decode_path(128, 64) == 'coop' and eng.decode_shape(128, 64) == (4, 1, 4)
     assert eng.decode_path(128, 128) == 'coop' and eng.decode_shape(128, 128) == (4, 1, 2)
     assert eng.decode_path(128, 256) == 'fused' and eng.decode_path(128, 512) == 'fused'
-    assert eng.decode_path(64, 64) == 'coop' and eng.decode_shape(64, 64) == (2, 1, 4)     # 64-row slabs (G = 2)
-    assert eng.decode_path(64, 128) == 'coop' and eng.decode_shape(64, 128) == (2, 1, 2)
-    assert eng.decode_path(64, 512) == 'fused' and eng.decode_shape(64, 512) == (2, 1, 1)
+    assert eng.decode_path(64, 64) == 'split'                  # 64-row slabs stay on the two-launch path ...
+    assert eng.decode_path(64, 512) == 'fused' and eng.decode_shape(64, 512) == (2, 1, 1)   # ... unless S = 1
     assert eng.decode_path(130, 64) == 'split'                 # B = 130 pads least with 64-row slabs
     eng.set_decode_split(0, 4)                                # forced 128-row slabs: two of them
     try:
@@ -87,19 +85,15 @@ def test_decode_path_rule(eng):
         eng.set_decode_split(0, 0)
 
 
-@pytest.mark.parametrize('B,P,G', [(128, 64, 4), (128, 128, 4), (130, 64, 4), (100, 3, 4), (64, 64, 2), (64, 128, 2),
-                                   (40, 3, 2), (100, 5, 2)],
-                         ids=['pop64_S4', 'pop128_S2', 'two_slabs_S2', 'ragged_3members', 'G2_pop64_S4', 'G2_pop128_S2',
-                              'G2_ragged_3members', 'G2_two_slabs_5members'])
-def test_coop_equals_split_and_oracle(eng, B, P, G):
-    """G = 4 (nicnes_decode_coop_kernel) and, since round 6, 64-row slabs (G = 2, nicnes_decode_coop2_kernel:
-    mscoco_nes.json's batch_size 64 at 64 / 128 members per GPU)"""
+@pytest.mark.parametrize('B,P', [(128, 64), (128, 128), (130, 64), (100, 3)],
+                         ids=['pop64_S4', 'pop128_S2', 'two_slabs_S2', 'ragged_3members'])
+def test_coop_equals_split_and_oracle(eng, B, P):
     dims = O.Dims()
     theta = O.make_theta(dims, 6, 4.0, 0.1)
     fc = _fc(B, 321 + B)
     _load(eng, theta, fc)
     if P < 8:
-        eng.set_decode_split(4, G)                # a few members: the automatic rule would split wider
+        eng.set_decode_split(4, 4)                # a few members: the automatic rule would split wider
     elif B > 128:
         eng.set_decode_split(0, 4)                # two 128-row slabs (the automatic rule takes 64-row ones)
     try:
@@ -141,9 +135,8 @@ def test_coop_bench_workload_fitness(eng):
             assert abs(fit[i, s] - f_ref) <= 1e-9 * max(1.0, f_ref)
 
 
-@pytest.mark.parametrize('G', [4, 2])
 @pytest.mark.parametrize('bias0', [40.0, 0.8])
-def test_coop_early_exit_matches_oracle(eng, bias0, G):
+def test_coop_early_exit_matches_oracle(eng, bias0):
     """rows emitting the end token at once, or staggered: every workgroup of the group leaves the
     launch at the same step (nets.py:242-243), the rest of the rows read zeros"""
     dims = O.Dims()
@@ -151,7 +144,7 @@ def test_coop_early_exit_matches_oracle(eng, bias0, G):
     theta[dims.offsets()['logit.bias'][0]] += np.float32(bias0)
     fc = _fc(130, 55)
     _load(eng, theta, fc)
-    eng.set_decode_split(4, G)
+    eng.set_decode_split(4, 4)
     try:
         assert eng.decode_path(130, 1) == 'coop'
         _, seq, lp = eng.evaluate(2, 0, 1, 0.0, return_seq=True, return_lp=True)
@@ -168,9 +161,6 @@ def test_coop_exact_pass_and_undecided_rows(monkeypatch):
     """the exact tie pass forced on every step (every workgroup of a group runs it), and the bounded
     lse widened so that many rows are undecided: tokens still match the oracle"""
     dims = O.Dims()
-    # (the widened margin with the bounded lse pinned on: the adaptive policy would run the G = 2 decode, after the
-    # G = 4 one's exact passes, on the exact sum, which has no undecided rows)
-    monkeypatch.setenv('NICNES_BOUNDED_LSE', '1')
     for env, val in (('NICNES_FORCE_EXACT', '1'), ('NICNES_LSE_MARGIN', '1e5')):
         monkeypatch.setenv(env, val)
         e = _engine(max_batch=64, max_members=2, seed=7)
@@ -178,18 +168,16 @@ def test_coop_exact_pass_and_undecided_rows(monkeypatch):
             theta = O.make_theta(dims, 0, 1.0, 0.0)
             fc = _fc(40, 99)
             _load(e, theta, fc)
-            for G in (4, 2):
-                e.set_decode_split(4, G)
-                assert e.decode_path(40, 2) == 'coop'
-                fb0 = e.stats()['tie_fallbacks']
-                _, seq = e.evaluate(3, 0, 2, SIGMA, return_seq=True)
-                seq = seq.cpu().numpy()
-                assert e.stats()['tie_fallbacks'] > fb0 and e.stats()['coop_timeouts'] == 0
-                idx = e.noise_indices(3, 0, 2).cpu().numpy()
-                for k in range(2):
-                    for s, sign in enumerate((+1, -1)):
-                        oseq, _, fr = O.decode(dims, O.perturb(theta, e._table_np, int(idx[k]), SIGMA, sign), fc)
-                        assert _mismatch(seq[k, s], oseq, fr) == [], (env, G, k, s)
+            e.set_decode_split(4, 4)
+            assert e.decode_path(40, 2) == 'coop'
+            _, seq = e.evaluate(3, 0, 2, SIGMA, return_seq=True)
+            seq = seq.cpu().numpy()
+            assert e.stats()['tie_fallbacks'] > 0 and e.stats()['coop_timeouts'] == 0
+            idx = e.noise_indices(3, 0, 2).cpu().numpy()
+            for k in range(2):
+                for s, sign in enumerate((+1, -1)):
+                    oseq, _, fr = O.decode(dims, O.perturb(theta, e._table_np, int(idx[k]), SIGMA, sign), fc)
+                    assert _mismatch(seq[k, s], oseq, fr) == [], (env, k, s)
         finally:
             e.close()
         monkeypatch.delenv(env)

@@ -2,7 +2,7 @@
 one member's step spread over S workgroups (vocabulary ranges for the logits, unit blocks for the
 cell) and 64-row slabs (G = 2) for batches of <= 64 images, against the C oracle. Every test runs
 twice: with the coop path on (nicnes_decode_coop_kernel takes the G = 4, S = 2 / 4 shapes in one
-launch, nicnes_decode_coop2_kernel the G = 2 ones) and off (two launches per step for every split shape).
+launch) and off (two launches per step for every split shape).
 
 Covers the shapes the automatic rule picks for BASELINE.json configs[1] (pop=64, B=128 -> S=4) and
 mscoco_nes.json's batch_size 64 (G=2), forced shapes from the fused kernel (G=4, S=1) up to S=16,
@@ -120,7 +120,7 @@ def test_pop64_auto_shape_tokens_and_fitness(eng, B, want):
     shape = eng.decode_shape(B, P)
     if eng.n_cu == 256:
         assert shape == want
-        assert eng.decode_path(B, P) == ('coop' if eng.coop_mode else 'split')
+        assert eng.decode_path(B, P) == ('coop' if (B == 128 and eng.coop_mode) else 'split')
     fit, seq = eng.evaluate(1, 0, P, SIGMA, return_seq=True)
     fit, seq = fit.cpu().numpy(), seq.cpu().numpy()
     idx = eng.noise_indices(1, 0, P).cpu().numpy()
