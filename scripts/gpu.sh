@@ -11,6 +11,7 @@
 #   ab      "SHAPES" [EXACT] [R]    one-process A/B of the decode builds in ablate_libs/ (scripts/ablate.py) per shape:
 #                                   512 512b64 64 128 64b64 512s
 #   libstats "VARIANTS" [POP] [R] [bench args]   rocprofv3 kernel stats of the bench with each ablate_libs/ library
+#   benchab "VARIANTS" R NAME [bench args]   bench lines with each ablate_libs/ library, R interleaved rounds
 #   prof    "POPS" [bench args]     kernel-trace stats + PMC passes (scripts/profile.sh)
 #   stats   NAME [bench args]       one rocprofv3 --kernel-trace --stats pass of a bench line
 set -eo pipefail
@@ -78,6 +79,18 @@ case $ACT in
   prof)
     POPS=${1:?POPS}; shift
     bash scripts/profile.sh $TAG "$POPS" "$@" ;;
+  benchab)
+    # bench lines of each ablate_libs/ library in turn, R interleaved rounds; NAME tags the workload
+    LIB=nes-img-captioning_amd/nicnes/libnicnes.so
+    V=${1:?VARIANTS}; R=${2:-2}; N=${3:?NAME}; shift 3
+    cp $LIB $O/product_lib.so
+    for r in $(seq 1 $R); do
+      for v in $V; do
+        cp ablate_libs/libnicnes_$v.so $LIB
+        timeout -k 10 200 $B "$@" > $O/${N}_${v}_$r.json 2> $O/${N}_${v}_$r.err
+      done
+    done
+    cp $O/product_lib.so $LIB && rm $O/product_lib.so ;;
   stats)
     N=${1:?NAME}; shift
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$N -o run --output-format csv -- \
